@@ -1,0 +1,443 @@
+"""Synthetic SwitchFL scenarios: square Flatland-format rail grids + trains + timetable.
+
+The reference builds its maps with Flatland's ``sparse_rail_generator`` /
+``sparse_line_generator`` (test_model.py:31-44, main.py:45-60), which are not
+installed here.  This module generates the same *kind* of input — a square
+grid of 16-bit Flatland cell transitions whose junctions are only the four
+switch classes SwitchFL accepts (switch_agents.py:262-267: (ports, routes) =
+(3,4) T/Y, (4,4) diamond, (4,6) single slip, (4,8) double slip), trains with
+start cell/heading, target station, earliest departure and latest arrival —
+deterministically from a seed.
+
+Conventions (Flatland's): headings/sides N=0, E=1, S=2, W=3; bit
+``15 - (4*heading + exit)`` of a cell's 16-bit word says a train *moving* in
+``heading`` may leave the cell through side ``exit`` (the ``dir_combo`` table
+of rail_graph.py:168-187).
+
+A cell is described by the set of undirected side pairs its rails connect;
+every pair is traversable both ways, so every intra-switch edge gets
+``rail_nodes=[]`` in the reference's port graph (rail_graph.py:222-235).
+
+The generator lays a Manhattan grid of track lines, removes a few boundary
+segments to hit the requested switch count, picks a junction layout per
+intersection, and retries until the (cell, heading) state graph is strongly
+connected (so every Flatland distance the reference evaluates in
+observer.compute_delay is finite — observer.py:35-36 raises otherwise).
+"""
+from __future__ import annotations
+
+import json
+import math
+from dataclasses import dataclass, field, asdict
+from typing import Dict, FrozenSet, List, Optional, Set, Tuple
+
+import numpy as np
+
+N, E, S, W = 0, 1, 2, 3
+DELTA = ((-1, 0), (0, 1), (1, 0), (0, -1))
+
+
+def opposite(d: int) -> int:
+    return (d + 2) % 4
+
+
+def pairs_to_bits(pairs) -> int:
+    """16-bit Flatland transition word of a cell from its undirected side pairs."""
+    bits = 0
+    for pr in pairs:
+        a, b = tuple(pr)
+        for enter_side, exit_side in ((a, b), (b, a)):
+            heading = opposite(enter_side)  # entering through side a means moving away from it
+            bits |= 1 << (15 - (4 * heading + exit_side))
+    return bits
+
+
+def transitions(word: int, heading: int) -> Tuple[int, int, int, int]:
+    """Exit bits (N, E, S, W) for a train moving in ``heading`` inside a cell."""
+    nib = (word >> ((3 - heading) * 4)) & 0xF
+    return ((nib >> 3) & 1, (nib >> 2) & 1, (nib >> 1) & 1, nib & 1)
+
+
+@dataclass
+class Train:
+    initial_position: Tuple[int, int]
+    initial_direction: int
+    target: Tuple[int, int]
+    earliest_departure: int = 0
+    latest_arrival: int = 0
+
+
+@dataclass
+class Scenario:
+    """Everything the hot path needs to (re)start an episode; the map is static."""
+    height: int
+    width: int
+    grid: List[List[int]]            # [H][W] 16-bit transition words
+    trains: List[Train]
+    max_episode_steps: int
+    malfunction_rate: float = 0.0
+    malfunction_min: int = 0
+    malfunction_max: int = 0
+    name: str = ""
+    seed: int = 0
+
+    # -- helpers ---------------------------------------------------------
+    def grid_array(self) -> np.ndarray:
+        return np.asarray(self.grid, dtype=np.int64)
+
+    def to_json(self) -> str:
+        d = asdict(self)
+        return json.dumps(d, sort_keys=True)
+
+    @staticmethod
+    def from_json(s: str) -> "Scenario":
+        d = json.loads(s)
+        trains = [Train(tuple(t["initial_position"]), int(t["initial_direction"]), tuple(t["target"]),
+                        int(t["earliest_departure"]), int(t["latest_arrival"])) for t in d.pop("trains")]
+        return Scenario(trains=trains, **d)
+
+    def save(self, path: str) -> None:
+        with open(path, "w") as f:
+            f.write(self.to_json())
+
+    @staticmethod
+    def load(path: str) -> "Scenario":
+        with open(path) as f:
+            return Scenario.from_json(f.read())
+
+    def with_malfunctions(self, rate: float, lo: int, hi: int) -> "Scenario":
+        d = Scenario.from_json(self.to_json())
+        d.malfunction_rate, d.malfunction_min, d.malfunction_max = float(rate), int(lo), int(hi)
+        return d
+
+
+# ---------------------------------------------------------------------------
+# state graph utilities (used for validation + timetable)
+# ---------------------------------------------------------------------------
+
+def _step_state(grid: np.ndarray, r: int, c: int, heading: int):
+    """All successor states (r', c', heading') of a train moving in ``heading`` at (r, c)."""
+    word = int(grid[r, c])
+    out = []
+    for e, ok in enumerate(transitions(word, heading)):
+        if ok:
+            dr, dc = DELTA[e]
+            out.append((r + dr, c + dc, e))
+    return out
+
+
+def rail_states(grid: np.ndarray):
+    H, W = grid.shape
+    res = []
+    for r in range(H):
+        for c in range(W):
+            if grid[r, c] == 0:
+                continue
+            for h in range(4):
+                if any(transitions(int(grid[r, c]), h)):
+                    res.append((r, c, h))
+    return res
+
+
+def strongly_connected(grid: np.ndarray) -> bool:
+    states = rail_states(grid)
+    if not states:
+        return False
+    idx = {s: i for i, s in enumerate(states)}
+    fwd = [[] for _ in states]
+    bwd = [[] for _ in states]
+    for s in states:
+        for t in _step_state(grid, *s):
+            if t not in idx:
+                return False  # leads off-rail / into a state with no exit
+            fwd[idx[s]].append(idx[t])
+            bwd[idx[t]].append(idx[s])
+
+    def reach(adj):
+        seen = [False] * len(states)
+        stack = [0]
+        seen[0] = True
+        while stack:
+            u = stack.pop()
+            for v in adj[u]:
+                if not seen[v]:
+                    seen[v] = True
+                    stack.append(v)
+        return all(seen)
+
+    return reach(fwd) and reach(bwd)
+
+
+def distance_to_cell(grid: np.ndarray, target: Tuple[int, int]) -> np.ndarray:
+    """BFS distance (in moves) from every (r, c, heading) state to ``target``; -1 = unreachable."""
+    H, W = grid.shape
+    dist = -np.ones((H, W, 4), dtype=np.int64)
+    tr, tc = target
+    # reverse adjacency on the fly: predecessor p of state (r,c,h) is any state whose move lands in (r,c) with heading h
+    from collections import deque
+    q = deque()
+    for h in range(4):
+        dist[tr, tc, h] = 0
+        q.append((tr, tc, h))
+    while q:
+        r, c, h = q.popleft()
+        # predecessor cell is one step against heading h
+        pr, pc = r - DELTA[h][0], c - DELTA[h][1]
+        if not (0 <= pr < H and 0 <= pc < W) or grid[pr, pc] == 0:
+            continue
+        for ph in range(4):
+            if transitions(int(grid[pr, pc]), ph)[h] and dist[pr, pc, ph] < 0:
+                dist[pr, pc, ph] = dist[r, c, h] + 1
+                q.append((pr, pc, ph))
+    return dist
+
+
+# ---------------------------------------------------------------------------
+# grid-of-lines network
+# ---------------------------------------------------------------------------
+
+def _junction_pairs(sides: Set[int], rng: np.random.Generator, slip_weights) -> FrozenSet[FrozenSet[int]]:
+    sides = sorted(sides)
+    if len(sides) == 2:
+        return frozenset({frozenset(sides)})
+    if len(sides) == 3:
+        trunk = sides[int(rng.integers(0, 3))]
+        others = [s for s in sides if s != trunk]
+        return frozenset({frozenset((trunk, others[0])), frozenset((trunk, others[1]))})
+    # four-way: diamond / single slip / double slip
+    straight = {frozenset((N, S)), frozenset((E, W))}
+    curves_a = [frozenset((W, S)), frozenset((E, N))]
+    curves_b = [frozenset((W, N)), frozenset((E, S))]
+    kind = rng.choice(3, p=slip_weights)
+    if kind == 0:
+        return frozenset(straight)
+    if kind == 1:
+        c = (curves_a + curves_b)[int(rng.integers(0, 4))]
+        return frozenset(straight | {c})
+    pick = curves_a if rng.integers(0, 2) == 0 else curves_b
+    return frozenset(straight | set(pick))
+
+
+def grid_network(nx_lines: int, ny_lines: int, spacing: int, margin: int, n_switches: int,
+                 rng: np.random.Generator, slip_weights=(0.2, 0.3, 0.5), size: Optional[int] = None):
+    """Lay out the line grid and return (grid words [H][W], set of junction cells)."""
+    span = (max(nx_lines, ny_lines) - 1) * spacing + 1
+    side_len = max(size or 0, 2 * margin + span)
+    rows = [margin + i * spacing for i in range(ny_lines)]
+    cols = [margin + j * spacing for j in range(nx_lines)]
+    seg = {}  # ((i,j),(i2,j2)) -> present
+    for i in range(ny_lines):
+        for j in range(nx_lines):
+            if j + 1 < nx_lines:
+                seg[((i, j), (i, j + 1))] = True
+            if i + 1 < ny_lines:
+                seg[((i, j), (i + 1, j))] = True
+
+    def sides_of(i, j):
+        s = set()
+        if seg.get(((i, j - 1), (i, j))):
+            s.add(W)
+        if seg.get(((i, j), (i, j + 1))):
+            s.add(E)
+        if seg.get(((i - 1, j), (i, j))):
+            s.add(N)
+        if seg.get(((i, j), (i + 1, j))):
+            s.add(S)
+        return s
+
+    def n_sw():
+        return sum(1 for i in range(ny_lines) for j in range(nx_lines) if len(sides_of(i, j)) >= 3)
+
+    # remove boundary segments between two boundary T junctions until the count matches
+    excess = n_sw() - n_switches
+    if excess < 0:
+        raise ValueError(f"grid {nx_lines}x{ny_lines} has only {n_sw()} switches < {n_switches}")
+    boundary = [k for k in seg if (k[0][0] == k[1][0] and k[0][0] in (0, ny_lines - 1)) or
+                (k[0][1] == k[1][1] and k[0][1] in (0, nx_lines - 1))]
+    order = list(rng.permutation(len(boundary)))
+    for bi in order:
+        if excess <= 0:
+            break
+        a, b = boundary[bi]
+        if not seg[(a, b)]:
+            continue
+        da, db = len(sides_of(*a)), len(sides_of(*b))
+        if excess >= 2 and da == 3 and db == 3:
+            seg[(a, b)] = False
+            excess -= 2
+    # odd remainder: drop an inward segment of a boundary T (T -> straight, 4-way -> T)
+    if excess == 1:
+        for (a, b), on in list(seg.items()):
+            if not on:
+                continue
+            ca, cb = len(sides_of(*a)), len(sides_of(*b))
+            ab = a[0] in (0, ny_lines - 1) or a[1] in (0, nx_lines - 1)
+            bb = b[0] in (0, ny_lines - 1) or b[1] in (0, nx_lines - 1)
+            if ab != bb and {ca, cb} == {3, 4}:
+                seg[(a, b)] = False
+                excess -= 1
+                break
+    if excess != 0 or n_sw() != n_switches:
+        raise ValueError("could not reach requested switch count")
+
+    pairs: Dict[Tuple[int, int], Set[FrozenSet[int]]] = {}
+    # plain track along present segments
+    for ((i, j), (i2, j2)), on in seg.items():
+        if not on:
+            continue
+        if i == i2:  # horizontal
+            r = rows[i]
+            for c in range(cols[j] + 1, cols[j2]):
+                pairs.setdefault((r, c), set()).add(frozenset((E, W)))
+        else:
+            c = cols[j]
+            for r in range(rows[i] + 1, rows[i2]):
+                pairs.setdefault((r, c), set()).add(frozenset((N, S)))
+    junctions = set()
+    for i in range(ny_lines):
+        for j in range(nx_lines):
+            sides = sides_of(i, j)
+            if len(sides) < 2:
+                if sides:
+                    raise ValueError("dead end produced")
+                continue
+            pairs[(rows[i], cols[j])] = set(_junction_pairs(sides, rng, slip_weights))
+            if len(sides) >= 3:
+                junctions.add((rows[i], cols[j]))
+    grid = np.zeros((side_len, side_len), dtype=np.int64)
+    for (r, c), prs in pairs.items():
+        grid[r, c] = pairs_to_bits(prs)
+    return grid, junctions
+
+
+def _first_switch_chain(grid: np.ndarray, junctions, pos, heading):
+    """Cells visited from ``pos`` (inclusive) until the first junction cell (inclusive)."""
+    r, c, h = pos[0], pos[1], heading
+    cells = [(r, c)]
+    for _ in range(grid.size + 1):
+        nxt = _step_state(grid, r, c, h)
+        if len(nxt) != 1:
+            raise ValueError("plain cell with != 1 exit")
+        r, c, h = nxt[0]
+        cells.append((r, c))
+        if (r, c) in junctions:
+            return cells
+    raise ValueError("no switch ahead")
+
+
+def timetable(path_lengths: List[int], width: int, height: int, n_cities: int, rs: np.random.RandomState):
+    """Earliest departure / latest arrival / max_episode_steps, restating the arithmetic of
+    flatland_patch/timetable_generators.py:44-136 (single-segment lines, speed 1)."""
+    num_agents = len(path_lengths)
+    max_episode_steps = int(4 * 2 * (width + height + (num_agents / n_cities)))
+    lengths = np.array(path_lengths, dtype=float)
+    mean_path_delay = float(np.mean(lengths)) * 0.2
+    new_steps = int(np.ceil(float(np.max(lengths)) * 1.5) + mean_path_delay)
+    old_steps = int(max_episode_steps * 3.0)
+    max_episode_steps = min(new_steps, old_steps)
+    end_buffer = int(max_episode_steps * 0.05)
+    latest_arrival_max = max_episode_steps - end_buffer
+    eds, las = [], []
+    for L in lengths:
+        travel_max = int(np.ceil(L * 1.3 + mean_path_delay))
+        window = max(latest_arrival_max - travel_max, 1)
+        ed = int(rs.randint(0, window))
+        eds.append(ed)
+        las.append(ed + travel_max)
+    return eds, las, max_episode_steps
+
+
+def generate(n_switches: int, n_trains: int, n_stations: int, seed: int, *,
+             nx_lines: Optional[int] = None, ny_lines: Optional[int] = None,
+             spacing: int = 5, margin: int = 3, size: Optional[int] = None,
+             malfunction: Tuple[float, int, int] = (0.0, 0, 0), name: str = "",
+             slip_weights=(0.2, 0.3, 0.5), max_tries: int = 200) -> Scenario:
+    """Deterministic scenario for (switch count, train count, station count, seed)."""
+    if nx_lines is None or ny_lines is None:
+        # smallest near-square line grid with nx*ny - 4 >= n_switches
+        best = None
+        for ny in range(2, 64):
+            for nx in range(ny, ny + 2):
+                if nx * ny - 4 >= n_switches and (best is None or nx * ny < best[0] * best[1]):
+                    best = (nx, ny)
+        nx_lines, ny_lines = best
+    rng = np.random.default_rng(seed)
+    for _ in range(max_tries):
+        grid, junctions = grid_network(nx_lines, ny_lines, spacing, margin, n_switches, rng,
+                                       slip_weights=slip_weights, size=size)
+        if not strongly_connected(grid):
+            continue
+        Hh, Ww = grid.shape
+        # candidate cells: straight plain cells not adjacent to a junction
+        plain = []
+        for r in range(Hh):
+            for c in range(Ww):
+                w = int(grid[r, c])
+                if w == 0 or (r, c) in junctions:
+                    continue
+                if w not in (pairs_to_bits({frozenset((E, W))}), pairs_to_bits({frozenset((N, S))})):
+                    continue
+                if any((r + dr, c + dc) in junctions for dr, dc in DELTA):
+                    continue
+                plain.append((r, c))
+        if len(plain) < n_trains + n_stations:
+            raise ValueError("map too small for trains + stations")
+        perm = rng.permutation(len(plain))
+        stations = [plain[i] for i in perm[:n_stations]]
+        starts_pool = [plain[i] for i in perm[n_stations:]]
+        dists = {s: distance_to_cell(grid, s) for s in stations}
+        trains: List[Train] = []
+        ok = True
+        for k in range(n_trains):
+            placed = False
+            for _try in range(50):
+                if not starts_pool:
+                    break
+                pos = starts_pool.pop(int(rng.integers(0, len(starts_pool))))
+                w = int(grid[pos])
+                heads = [h for h in range(4) if any(transitions(w, h))]
+                h0 = heads[int(rng.integers(0, len(heads)))]
+                tgt = stations[int(rng.integers(0, n_stations))]
+                chain = _first_switch_chain(grid, junctions, pos, h0)
+                if tgt in chain:
+                    continue
+                if dists[tgt][pos[0], pos[1], h0] < 0:
+                    continue
+                trains.append(Train((int(pos[0]), int(pos[1])), int(h0), (int(tgt[0]), int(tgt[1]))))
+                placed = True
+                break
+            if not placed:
+                ok = False
+                break
+        if not ok:
+            continue
+        trains.sort(key=lambda t: (t.initial_position[0], t.initial_position[1], t.initial_direction))
+        # shortest path lengths in waypoints (Flatland's len(path) counts start and target)
+        lens = [int(dists[t.target][t.initial_position[0], t.initial_position[1], t.initial_direction]) + 1
+                for t in trains]
+        rs = np.random.RandomState(seed & 0x7FFFFFFF)
+        eds, las, mes = timetable(lens, Ww, Hh, max(2, n_stations), rs)
+        for t, ed, la in zip(trains, eds, las):
+            t.earliest_departure, t.latest_arrival = ed, la
+        return Scenario(height=Hh, width=Ww, grid=[[int(x) for x in row] for row in grid], trains=trains,
+                        max_episode_steps=int(mes), malfunction_rate=float(malfunction[0]),
+                        malfunction_min=int(malfunction[1]), malfunction_max=int(malfunction[2]),
+                        name=name, seed=int(seed))
+    raise RuntimeError("could not generate a strongly connected scenario")
+
+
+# Named configurations (BASELINE.json configs)
+CONFIGS = {
+    # C1: stands in for test_model.py's 18x18 / 5 cities / 2 trains map (Flatland's own map is unobtainable offline)
+    "c1": dict(n_switches=5, n_trains=2, n_stations=2, nx_lines=3, ny_lines=3, spacing=6, margin=2, size=18),
+    "c2": dict(n_switches=16, n_trains=8, n_stations=4, nx_lines=5, ny_lines=4, spacing=5, margin=2),
+    "c3": dict(n_switches=64, n_trains=32, n_stations=8, nx_lines=9, ny_lines=8, spacing=5, margin=3),
+    "c5": dict(n_switches=256, n_trains=128, n_stations=16, nx_lines=17, ny_lines=16, spacing=5, margin=3),
+}
+
+MAP_SEED = 450565  # the reference default seed (test_model.py:30)
+
+
+def make_config(name: str, seed: int = MAP_SEED, malfunction=(0.01, 5, 15)) -> Scenario:
+    kw = dict(CONFIGS[name])
+    return generate(seed=seed, malfunction=malfunction, name=name, **kw)
