@@ -1,0 +1,146 @@
+"""Benchmark: agent-env-steps/sec of the SwitchFL + network-distributed-Q hot path on MI355X.
+
+Workload (BASELINE.json configs[2]): the 64-switch / 32-train map, 65,536 lock-step envs per GPU,
+learning mode (epsilon-greedy, Q updates) with the hyper-parameters of test_model.py:56-63 and
+malfunctions at rate 0.01 (5-15 ticks, test_model.py:14-18).  A *step* = every env advances by
+``--decisions`` agent-env-steps (one iteration of distr_q.py:302-362 each, with every Flatland
+tick in between and episodes restarting as they end).  N GPUs: one process per GPU, each with its
+own 65,536 envs (weak scaling, no collective on the data path; the reference's parallelism is an
+embarrassingly parallel seed sweep, hyperparam_tuning.py:85-91).
+
+Usage: python bench.py [--gpus N --steps K --warmup W]; N > 1 is launched by torch.distributed.run.
+"""
+from __future__ import annotations
+
+import argparse
+import importlib
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+PKG = "network-distributed-q-learning_amd"
+
+HP = dict(gamma=1.0, epsilon=0.5, epsilon_decay_rate=0.9997, lr=0.1, lr_decay_rate=1.0, default_q=0.0)
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+METRIC = "agent-env-steps/sec (whole node), 64-switch map, 1/2/4/8 MI355X vs CPU"
+
+
+def cpu_baseline(sc, seconds: float):
+    """The CPU oracle (pure-Python restatement of the reference loop), one env, one core."""
+    from oracle import sfl_oracle as so
+    env, model = so.build(sc, 450565, HP, trace=False)
+    state = None
+    n = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        n += 100
+        state = so.run_decisions(model, n, state)
+    dt = time.perf_counter() - t0
+    return dict(value=n / dt, unit="agent-env-steps/sec", cores=1, kind="port",
+                sample=f"oracle/sfl_oracle.py learn loop, 1 env of the c3 map, {n} decisions in {dt:.1f} s "
+                       f"(from episode start, incl. the Q-table init)")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--decisions", type=int, default=64, help="agent-env-steps per env per step")
+    ap.add_argument("--envs", type=int, default=65536, help="envs per GPU")
+    ap.add_argument("--config", default="c3")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    else:
+        torch.cuda.set_device(0)
+
+    mapgen = importlib.import_module(PKG + ".mapgen")
+    comp = importlib.import_module(PKG + ".compiler")
+    runtime = importlib.import_module(PKG + ".runtime")
+    sc = mapgen.make_config(args.config)
+    cm = comp.compile_scenario(sc)
+    E = args.envs
+    seeds = [450565 + rank * E + i for i in range(E)]
+    b = runtime.Batch(cm, HP, seeds, device=local)
+    b.learn_begin()
+    b.apply_qinit()
+    for _ in range(args.warmup):
+        b.step(args.decisions)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    barrier()
+    t0 = time.perf_counter()
+    total = 0
+    kms = 0.0
+    abytes = 0
+    for _ in range(args.steps):
+        n, ms = b.step(args.decisions)
+        total += n
+        kms += ms
+        abytes += b.counters()["last_launch_alg_bytes"]
+    barrier()
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([dt, float(total)], dtype=torch.float64, device="cuda")
+        mx = t.clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        sm = t.clone()
+        dist.all_reduce(sm, op=dist.ReduceOp.SUM)
+        dt, total_all = float(mx[0]), float(sm[1])
+    else:
+        total_all = float(total)
+    if rank == 0:
+        avg_ms = kms / max(1, args.steps)
+        bytes_per_launch = abytes / max(1, args.steps)
+        achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+        res = {
+            "metric": METRIC,
+            "value": total_all / dt,
+            "unit": "agent-env-steps/sec",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": dt * 1e3 / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic 64-switch/32-train Flatland-format map (mapgen c3, seed 450565), random-init "
+                    "(default_q + optimistic init) Q-tables",
+            "config": {"workload": f"{args.config}: {cm.S} switches / {cm.T} trains, {E} envs per GPU, learning "
+                                   f"(eps-greedy + Q update), {args.decisions} agent-env-steps per env per step",
+                       "envs_per_gpu": E, "decisions_per_env_per_step": args.decisions,
+                       "parallelism": f"env-batch dp{world}"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "kernel": "k_run", "avg_kernel_ms": avg_ms,
+                         "alg_bytes_per_launch": bytes_per_launch},
+        }
+        if world == 1 and not args.no_cpu:
+            res["cpu_baseline"] = cpu_baseline(sc, args.cpu_seconds)
+        print(json.dumps(res), flush=True)
+    b.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

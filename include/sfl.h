@@ -1,0 +1,145 @@
+/*
+ * sfl.h — C-ABI of the MI355X SwitchFL / network-distributed Q-learning hot path.
+ *
+ * One handle = one batch of E lock-step SwitchFL environments (all on the same
+ * compiled map, each with its own seed, its own tabular Q-table and its own RNG
+ * stream) resident in the HBM of one GPU.  Plain pointers and sizes only; no
+ * torch types.  Every function returns 0 on success and -1 on failure, with the
+ * message in sfl_last_error() (thread-local).  Calls are synchronous: they
+ * return after the device work they launched has completed.  One handle is used
+ * from one host thread.  Multi-GPU = one process and one handle per device.
+ *
+ * The interfaces these entry points replace in the reference
+ * (AI4REALNET/network-distributed-q-learning):
+ *
+ *   sfl_create        ASyncSwitchEnv(rail_env, max_steps=...)        switchfl/switch_env.py:605-614
+ *                     + DistrQLearning(env, gamma, epsilon, ...)     switchfl/distr_q.py:32-45
+ *                     (RailNetwork(rail_env) graph compile is done on the host:
+ *                      network-distributed-q-learning_amd/compiler.py)
+ *   sfl_learn_begin   rng = np.random.default_rng(self.seed),
+ *                     agent_num_interactions = {...: 0}               switchfl/distr_q.py:263, 269
+ *   sfl_apply_qinit   DistrQLearning.__init_q_table                  switchfl/distr_q.py:81-181, 299-300
+ *   sfl_learn         the episode loop of DistrQLearning.learn        switchfl/distr_q.py:275-366
+ *   sfl_test          DistrQLearning.test (greedy episode)           switchfl/distr_q.py:184-241
+ *   sfl_step          `decisions` iterations of the agent_iter loop  switchfl/distr_q.py:302-362
+ *                     (learning mode, episodes restart as they end; the benchmark step)
+ *   sfl_get_q / sfl_set_q   DistrQLearning.q_table / save / load     switchfl/distr_q.py:492-527
+ *   sfl_get_counters  timing/progress accumulators                   switchfl/switch_env.py:67-73
+ */
+#ifndef SFL_H
+#define SFL_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SFL_ABI_VERSION 1
+
+typedef struct sfl_handle sfl_handle;
+
+/* Compiled map (all arrays are host pointers; the library copies them).
+ * Layouts are produced by compiler.py; see DESIGN.md "HBM layout". */
+typedef struct {
+  int32_t H, W;               /* grid size (square) */
+  int32_t S, T, K;            /* switches, trains, distinct target stations */
+  int32_t max_episode_steps;  /* Flatland timetable horizon */
+  double mf_rate;             /* malfunction rate per train per tick */
+  int32_t mf_min, mf_max;     /* malfunction duration bounds */
+  uint64_t q_per_env;         /* doubles of compact Q-table per env */
+  uint32_t rows_per_env;      /* Q rows per env (key-set bitmap) */
+  const uint16_t* grid;       /* [H*W] 16-bit Flatland transitions */
+  const int16_t* cell_sw;     /* [H*W] switch index or -1 */
+  const uint8_t* sw_np;       /* [S] ports */
+  const uint8_t* sw_na;       /* [S] actions incl. STOP */
+  const uint8_t* act_src;     /* [S*8] route action -> source port slot */
+  const uint8_t* act_dst;     /* [S*8] route action -> destination port slot */
+  const uint8_t* act_turn;    /* [S*8] second rail action (1 left, 2 forward, 3 right) */
+  const uint8_t* act_j;       /* [S*8] index of the action inside its source slot's compact row */
+  const uint8_t* first_other; /* [4S] first action not leaving from this slot */
+  const uint8_t* port_side;   /* [4S] map_direction(port) */
+  const uint8_t* slot_nroutes;/* [4S] routes leaving from this slot */
+  const uint8_t* slot_route_act; /* [4S*4] their action indices */
+  const uint8_t* q_w;         /* [4S] compact row width = routes + 1 (STOP) */
+  const int16_t* port_nb;     /* [4S] rail neighbour port (global id 4*switch+slot) */
+  const int16_t* port_len;    /* [4S] plain cells between the two ports */
+  const int16_t* port_unique; /* [4S] unique onward port of a target port, or -1 */
+  const uint64_t* q_off;      /* [4S] offset (doubles) of the (switch, in-slot) block */
+  const uint32_t* row_base;   /* [4S] first row id of the block */
+  const int32_t* dist;        /* [K*H*W*4] distance to station, 0x3FFFFFFF = inf */
+  const int32_t* tr_ed;       /* [T] earliest departure */
+  const int32_t* tr_la;       /* [T] latest arrival */
+  const int32_t* tr_k;        /* [T] target station */
+  const int32_t* tr_target;   /* [T] target cell */
+  const int32_t* tr_init_cell;/* [T] start cell */
+  const int32_t* tr_init_dist;/* [T] cells to the first switch port */
+  const int32_t* tr_init_delay; /* [T] delay at reset */
+  const uint8_t* tr_init_dir; /* [T] start heading */
+  const int16_t* tr_init_port;/* [T] first switch port */
+} sfl_map_desc;
+
+typedef struct {
+  double gamma, epsilon, epsilon_decay_rate, lr, lr_decay_rate, default_q;
+  int64_t max_steps;          /* ASyncSwitchEnv max_steps (truncation) */
+  int32_t ntab;               /* length of the two tables below */
+  const double* eps_tab;      /* epsilon * decay**n, Python float arithmetic */
+  const double* lr_tab;       /* lr * lr_decay**n */
+} sfl_hparams;
+
+typedef struct {
+  int32_t n_episodes;         /* episodes to run in this call (learn: learning episodes) */
+  int32_t exploit_freq;       /* learn: greedy round before episode t when (t+1) % f == 0 (0 = off) */
+  int32_t stats_cap;          /* rows of the output buffers below (>= n_episodes to keep all) */
+  int32_t pad_;
+  /* optional host outputs, row = episode index % stats_cap, [row][env] ([row][train][env] for delays) */
+  double* cum_reward;
+  int32_t* arrived;
+  int32_t* malfunctions;
+  int32_t* decisions;
+  int32_t* ticks;
+  int32_t* delays;
+  double* exploit_cum;
+  int32_t* exploit_arrived;
+  /* optional per-decision trace of one env (debug / parity tests): [trace_cap][4] uint64 */
+  uint64_t* trace;
+  uint64_t* trace_n;
+  int32_t trace_env;
+  int32_t trace_cap;
+} sfl_run_args;
+
+typedef struct {
+  uint64_t decisions;         /* agent-env-steps over all envs since create */
+  uint64_t last_launch_decisions;
+  uint64_t last_launch_ticks;
+  uint64_t last_launch_alg_bytes; /* sum of 220+48P+8A per decision + 36*T_live per env-tick */
+  double last_kernel_ms;      /* device time of the last run/step launch (HIP events) */
+} sfl_counters;
+
+int sfl_abi_version(void);
+const char* sfl_last_error(void);
+int sfl_device_count(int* n);
+
+int sfl_create(const sfl_map_desc* map, const sfl_hparams* hp, uint32_t n_envs, const uint64_t* env_seeds,
+               int device, sfl_handle** out);
+int sfl_destroy(sfl_handle* h);
+
+int sfl_learn_begin(sfl_handle* h, const uint64_t* rng_states /* [n_envs][5] */);
+int sfl_apply_qinit(sfl_handle* h, uint32_t n_rows, const uint32_t* row_port, const uint32_t* row_state,
+                    const double* values /* [n_rows][4], NaN = default_q */);
+int sfl_mark_exploit_done(sfl_handle* h);
+int sfl_learn(sfl_handle* h, sfl_run_args* args);
+int sfl_test(sfl_handle* h, sfl_run_args* args);
+int sfl_step(sfl_handle* h, int64_t decisions_per_env, uint64_t* decisions_done, double* kernel_ms);
+
+int sfl_get_q(sfl_handle* h, uint32_t env, double* q /* [q_per_env] */, uint32_t* touched /* [(rows+31)/32] */);
+int sfl_set_q(sfl_handle* h, uint32_t env, const double* q, const uint32_t* touched);
+int sfl_get_counters(sfl_handle* h, sfl_counters* out);
+/* read back one env's state word arrays (debug / parity tests) */
+int sfl_get_env_state(sfl_handle* h, uint32_t env, int32_t* elapsed, int32_t* phase, uint64_t* sem /* [4S] */,
+                      int32_t* tr_pos /* [T] */, uint32_t* tr_bits /* [T] */);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SFL_H */

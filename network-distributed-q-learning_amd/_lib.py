@@ -1,0 +1,118 @@
+"""ctypes binding of include/sfl.h.
+
+The product loads ``libsfl.so`` (built for gfx950 by build.py) and nothing else:
+there is no CPU fallback.  ``load(path)`` also serves the test-only host build
+(``libsfl_hostsim.so``), which tests/ use to check the kernel body against the
+oracle without a GPU.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+PRODUCT_LIB = os.path.join(HERE, "libsfl.so")
+
+P = C.POINTER
+
+
+class MapDesc(C.Structure):
+    _fields_ = [
+        ("H", C.c_int32), ("W", C.c_int32), ("S", C.c_int32), ("T", C.c_int32), ("K", C.c_int32),
+        ("max_episode_steps", C.c_int32), ("mf_rate", C.c_double), ("mf_min", C.c_int32), ("mf_max", C.c_int32),
+        ("q_per_env", C.c_uint64), ("rows_per_env", C.c_uint32),
+        ("grid", P(C.c_uint16)), ("cell_sw", P(C.c_int16)),
+        ("sw_np", P(C.c_uint8)), ("sw_na", P(C.c_uint8)), ("act_src", P(C.c_uint8)), ("act_dst", P(C.c_uint8)),
+        ("act_turn", P(C.c_uint8)), ("act_j", P(C.c_uint8)), ("first_other", P(C.c_uint8)),
+        ("port_side", P(C.c_uint8)), ("slot_nroutes", P(C.c_uint8)), ("slot_route_act", P(C.c_uint8)),
+        ("q_w", P(C.c_uint8)), ("port_nb", P(C.c_int16)), ("port_len", P(C.c_int16)), ("port_unique", P(C.c_int16)),
+        ("q_off", P(C.c_uint64)), ("row_base", P(C.c_uint32)), ("dist", P(C.c_int32)),
+        ("tr_ed", P(C.c_int32)), ("tr_la", P(C.c_int32)), ("tr_k", P(C.c_int32)), ("tr_target", P(C.c_int32)),
+        ("tr_init_cell", P(C.c_int32)), ("tr_init_dist", P(C.c_int32)), ("tr_init_delay", P(C.c_int32)),
+        ("tr_init_dir", P(C.c_uint8)), ("tr_init_port", P(C.c_int16)),
+    ]
+
+
+class HParams(C.Structure):
+    _fields_ = [
+        ("gamma", C.c_double), ("epsilon", C.c_double), ("epsilon_decay_rate", C.c_double), ("lr", C.c_double),
+        ("lr_decay_rate", C.c_double), ("default_q", C.c_double), ("max_steps", C.c_int64), ("ntab", C.c_int32),
+        ("eps_tab", P(C.c_double)), ("lr_tab", P(C.c_double)),
+    ]
+
+
+class RunArgs(C.Structure):
+    _fields_ = [
+        ("n_episodes", C.c_int32), ("exploit_freq", C.c_int32), ("stats_cap", C.c_int32), ("pad_", C.c_int32),
+        ("cum_reward", P(C.c_double)), ("arrived", P(C.c_int32)), ("malfunctions", P(C.c_int32)),
+        ("decisions", P(C.c_int32)), ("ticks", P(C.c_int32)), ("delays", P(C.c_int32)),
+        ("exploit_cum", P(C.c_double)), ("exploit_arrived", P(C.c_int32)),
+        ("trace", P(C.c_uint64)), ("trace_n", P(C.c_uint64)), ("trace_env", C.c_int32), ("trace_cap", C.c_int32),
+    ]
+
+
+class Counters(C.Structure):
+    _fields_ = [("decisions", C.c_uint64), ("last_launch_decisions", C.c_uint64),
+                ("last_launch_ticks", C.c_uint64), ("last_launch_alg_bytes", C.c_uint64),
+                ("last_kernel_ms", C.c_double)]
+
+
+EXPORTS = {
+    "sfl_abi_version": (C.c_int, []),
+    "sfl_last_error": (C.c_char_p, []),
+    "sfl_device_count": (C.c_int, [P(C.c_int)]),
+    "sfl_create": (C.c_int, [P(MapDesc), P(HParams), C.c_uint32, P(C.c_uint64), C.c_int, P(C.c_void_p)]),
+    "sfl_destroy": (C.c_int, [C.c_void_p]),
+    "sfl_learn_begin": (C.c_int, [C.c_void_p, P(C.c_uint64)]),
+    "sfl_apply_qinit": (C.c_int, [C.c_void_p, C.c_uint32, P(C.c_uint32), P(C.c_uint32), P(C.c_double)]),
+    "sfl_mark_exploit_done": (C.c_int, [C.c_void_p]),
+    "sfl_learn": (C.c_int, [C.c_void_p, P(RunArgs)]),
+    "sfl_test": (C.c_int, [C.c_void_p, P(RunArgs)]),
+    "sfl_step": (C.c_int, [C.c_void_p, C.c_int64, P(C.c_uint64), P(C.c_double)]),
+    "sfl_get_q": (C.c_int, [C.c_void_p, C.c_uint32, P(C.c_double), P(C.c_uint32)]),
+    "sfl_set_q": (C.c_int, [C.c_void_p, C.c_uint32, P(C.c_double), P(C.c_uint32)]),
+    "sfl_get_counters": (C.c_int, [C.c_void_p, P(Counters)]),
+    "sfl_get_env_state": (C.c_int, [C.c_void_p, C.c_uint32, P(C.c_int32), P(C.c_int32), P(C.c_uint64),
+                                    P(C.c_int32), P(C.c_uint32)]),
+}
+
+
+class SflError(RuntimeError):
+    pass
+
+
+class Lib:
+    def __init__(self, path: str):
+        if not os.path.exists(path):
+            raise SflError(f"{path} not found — build it first (python -c 'import __graft_entry__ as g; g.build()')")
+        self.path = path
+        self.dll = C.CDLL(path)
+        for name, (res, args) in EXPORTS.items():
+            fn = getattr(self.dll, name)
+            fn.restype = res
+            fn.argtypes = args
+        if self.dll.sfl_abi_version() != 1:
+            raise SflError("ABI version mismatch")
+
+    def check(self, rc: int, what: str):
+        if rc != 0:
+            raise SflError(f"{what}: {self.dll.sfl_last_error().decode(errors='replace')}")
+
+    def device_count(self) -> int:
+        n = C.c_int(0)
+        self.dll.sfl_device_count(C.byref(n))
+        return n.value
+
+
+_product = None
+
+
+def load_product() -> Lib:
+    """The HIP library; raises if it is missing or no GPU is visible (no fallback)."""
+    global _product
+    if _product is None:
+        lib = Lib(PRODUCT_LIB)
+        if lib.device_count() < 1:
+            raise SflError("libsfl.so loaded but no HIP device is visible: the SwitchFL hot path runs on MI355X only")
+        _product = lib
+    return _product

@@ -1,0 +1,49 @@
+"""Build the HIP library in-tree (and, for tests, the host build of the same kernel body)."""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = os.environ.get("SFL_ARCH", "gfx950")
+SOURCES = ["sfl.hip", "sfl_core.h", "sfl_rng.h", "sfl_engine.h", "sfl_capi.inc", "sfl_hostsim.cpp",
+           os.path.join("..", "..", "include", "sfl.h")]
+
+
+def _stale(out: str, srcs) -> bool:
+    if not os.path.exists(out):
+        return True
+    t = os.path.getmtime(out)
+    return any(os.path.getmtime(os.path.join(CSRC, s)) > t for s in srcs)
+
+
+def build_hip(force: bool = False, verbose: bool = False) -> str:
+    out = os.path.join(HERE, "libsfl.so")
+    if force or _stale(out, SOURCES):
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off",
+               "-Wno-unused-result", "-Wno-unused-value", "-o", out + ".tmp", os.path.join(CSRC, "sfl.hip")]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True, cwd=CSRC)
+        os.replace(out + ".tmp", out)
+    return out
+
+
+def build_hostsim(out_dir: str = None, force: bool = False) -> str:
+    """TEST ONLY: the same kernel body compiled for the host CPU (libsfl_hostsim.so)."""
+    out_dir = out_dir or os.path.join(HERE, "..", "build")
+    os.makedirs(out_dir, exist_ok=True)
+    out = os.path.abspath(os.path.join(out_dir, "libsfl_hostsim.so"))
+    if force or _stale(out, SOURCES):
+        cmd = ["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-fopenmp",
+               "-o", out + ".tmp", os.path.join(CSRC, "sfl_hostsim.cpp")]
+        subprocess.run(cmd, check=True, cwd=CSRC)
+        os.replace(out + ".tmp", out)
+    return out
+
+
+if __name__ == "__main__":
+    print(build_hip(force="--force" in sys.argv, verbose=True))

@@ -1,0 +1,122 @@
+// MI355X (gfx950) build of the SwitchFL hot path: libsfl.so.
+//
+// One thread = one environment (sfl_core.h env_run).  A block of 256 threads is
+// 4 waves; at 65,536 envs the grid is 256 blocks = one per CU, one wave per
+// SIMD.  Envs are independent, so there is no inter-workgroup communication;
+// the static map tables (a few hundred KB) are read by every CU and stay in
+// L2 / the Infinity Cache.  Build: see build.py (hipcc --offload-arch=gfx950
+// -O3 -ffp-contract=off: the Q update must be the reference's separate f64
+// multiply/add, not a contracted FMA).
+#include <hip/hip_runtime.h>
+
+#include <string>
+
+#include "sfl_engine.h"
+
+namespace {
+
+__global__ void __launch_bounds__(256) k_run(sfl::SflMap m, sfl::SflState s, sfl::SflCtl c) {
+  const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < s.E) sfl::env_run(m, s, c, e);
+}
+
+__global__ void k_fill_f64(double* p, double v, size_t n) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) p[i] = v;
+}
+
+// one thread per (env, patch row); consecutive threads = consecutive rows of one env
+__global__ void k_qinit(sfl::SflMap m, sfl::SflState s, uint32_t n_rows, const uint32_t* port, const uint32_t* state,
+                        const double* vals) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (size_t)n_rows * s.E) return;
+  const uint32_t e = (uint32_t)(i / n_rows), r = (uint32_t)(i % n_rows);
+  const uint32_t g = port[r], st = state[r];
+  const int w = m.q_w[g];
+  double* row = s.q + (size_t)e * m.q_per_env + m.q_off[g] + (size_t)st * w;
+  for (int j = 0; j < w; ++j) {
+    const double v = vals[(size_t)r * 4 + j];
+    row[j] = (v != v) ? m.default_q : v;
+  }
+  const uint32_t rid = m.row_base[g] + st;
+  atomicOr(&s.touched[(size_t)e * m.touched_words + (rid >> 5)], 1u << (rid & 31u));
+}
+
+struct HipBackend {
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  std::string err;
+  int dev = 0;
+
+  static int device_count(int* n) {
+    int c = 0;
+    if (hipGetDeviceCount(&c) != hipSuccess) c = 0;
+    *n = c;
+    return 0;
+  }
+  bool check(hipError_t rc, const char* what) {
+    if (rc == hipSuccess) return true;
+    if (err.empty()) err = std::string(what) + ": " + hipGetErrorString(rc);
+    return false;
+  }
+  const char* error() const { return err.c_str(); }
+  int init(int device) {
+    dev = device;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) {
+      err = "no HIP device visible (this library needs an MI355X)";
+      return -1;
+    }
+    if (!check(hipSetDevice(device), "hipSetDevice")) return -1;
+    if (!check(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking), "hipStreamCreate")) return -1;
+    if (!check(hipEventCreate(&ev0), "hipEventCreate") || !check(hipEventCreate(&ev1), "hipEventCreate")) return -1;
+    return 0;
+  }
+  ~HipBackend() {
+    if (ev0) hipEventDestroy(ev0);
+    if (ev1) hipEventDestroy(ev1);
+    if (stream) hipStreamDestroy(stream);
+  }
+  void* alloc(size_t bytes) {
+    void* p = nullptr;
+    if (!check(hipMalloc(&p, bytes), "hipMalloc")) return nullptr;
+    return p;
+  }
+  void free(void* p) {
+    if (p) hipFree(p);
+  }
+  void h2d(void* d, const void* s, size_t n) { check(hipMemcpyAsync(d, s, n, hipMemcpyHostToDevice, stream), "h2d"); }
+  void d2h(void* d, const void* s, size_t n) {
+    check(hipMemcpyAsync(d, s, n, hipMemcpyDeviceToHost, stream), "d2h");
+    check(hipStreamSynchronize(stream), "d2h sync");
+  }
+  void memset(void* p, int v, size_t n) { check(hipMemsetAsync(p, v, n, stream), "memset"); }
+  void fill_f64(double* p, double v, size_t n) {
+    k_fill_f64<<<4096, 256, 0, stream>>>(p, v, n);
+    check(hipGetLastError(), "k_fill_f64");
+  }
+  void qinit(const sfl::SflMap& m, const sfl::SflState& s, uint32_t n_rows, const uint32_t* port,
+             const uint32_t* state, const double* vals) {
+    const size_t n = (size_t)n_rows * s.E;
+    const unsigned blocks = (unsigned)((n + 255) / 256);
+    k_qinit<<<blocks, 256, 0, stream>>>(m, s, n_rows, port, state, vals);
+    check(hipGetLastError(), "k_qinit");
+  }
+  int run(const sfl::SflMap& m, const sfl::SflState& s, const sfl::SflCtl& c, float* ms) {
+    const unsigned blocks = (s.E + 255) / 256;
+    check(hipEventRecord(ev0, stream), "event");
+    k_run<<<blocks, 256, 0, stream>>>(m, s, c);
+    if (!check(hipGetLastError(), "k_run launch")) return -1;
+    check(hipEventRecord(ev1, stream), "event");
+    if (!check(hipEventSynchronize(ev1), "k_run")) return -1;
+    float t = 0.f;
+    hipEventElapsedTime(&t, ev0, ev1);
+    *ms = t;
+    return err.empty() ? 0 : -1;
+  }
+  int sync() { return check(hipStreamSynchronize(stream), "sync") && err.empty() ? 0 : -1; }
+};
+
+}  // namespace
+
+using Backend = HipBackend;
+#include "sfl_capi.inc"

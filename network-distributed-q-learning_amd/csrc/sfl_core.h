@@ -1,0 +1,1091 @@
+// SwitchFL + network-distributed Q-learning: one lock-step environment per lane.
+//
+// This header is the whole hot path, written once
+// as host/device code.  The HIP kernel (sfl.hip) runs ``env_run`` with one
+// thread per environment; tests also compile it for the host (sfl_hostsim.cpp)
+// to check it against the CPU oracle without a GPU.  Reference behaviour it
+// restates, with citations at each function:
+//   switchfl/distr_q.py        learn / test / update / max_q / max_action
+//   switchfl/switch_env.py     reset / _apply_action / _move_trains / _check_active_switch
+//   switchfl/rail_network.py   transition_train / transition_semaphore / extend_semaphores
+//   switchfl/observer.py       check_port_blocked / compute_delay / observe
+//   switchfl/reward_func.py    StandardRewardFunction
+//   oracle/flatland_lite.py    the frozen Flatland RailEnv.step spec
+//
+// Memory layout (DESIGN.md §"HBM layout"): every per-env quantity is SoA with
+// the env index fastest (``field[i * E + e]``) so a wave's 64 lanes touching
+// the same field of their own envs coalesce; the Q-table is env-major (one
+// contiguous block per env) because rows are gathered at data-dependent
+// offsets.
+#pragma once
+#include <stdint.h>
+#include "sfl_rng.h"
+
+#if !defined(__HIPCC__)
+#include <math.h>
+#endif
+
+namespace sfl {
+
+enum : uint32_t { A_NOTHING = 0, A_LEFT = 1, A_FWD = 2, A_RIGHT = 3, A_STOP = 4, A_NONE = 15 };
+enum : uint32_t { S_WAITING = 0, S_READY = 1, S_MF_OFF = 2, S_MOVING = 3, S_STOPPED = 4, S_MALF = 5, S_DONE = 6 };
+enum : int32_t { PH_RESET = 0, PH_TICK = 1, PH_DECIDE = 2, PH_POST = 3, PH_END = 4 };
+enum : uint32_t { F_TERM = 1, F_TRUNC = 2, F_GREEDY = 4, F_EXPLOIT_DONE = 8, F_OWN_SCAN = 16, F_INFLIGHT = 32 };
+enum : uint32_t {
+  E_INF_DIST = 1,      // observer.py:35-36 would raise ValueError
+  E_PLAN_OVF = 2,      // train plan longer than the packed ring
+  E_PORT = 4,          // active train's next port not at the deciding switch (observer.py:294-301)
+  E_BAD_ACTION = 8,    // action outside the switch's action space (switch_env.py:213-215)
+};
+
+constexpr int32_t DIST_INF = 0x3FFFFFFF;
+constexpr int OWN_MAX = 16;
+constexpr int MAXW = 4;  // train bitmask words (T <= 128)
+constexpr uint32_t PEND_NONE = 0xFFFFFFFFu;
+constexpr uint16_t PORT_NONE = 0xFFFFu;
+
+struct SflMap {
+  int32_t H, W, S, T, K, NP;
+  int32_t max_episode_steps, mf_min, mf_max, ntab;
+  double mf_rate, gamma, eps0, eps_decay, lr0, lr_decay, default_q;
+  int64_t max_steps;
+  uint64_t q_per_env;
+  uint32_t rows_per_env, touched_words;
+  const uint16_t* grid;
+  const int16_t* cell_sw;
+  const uint8_t* sw_np;
+  const uint8_t* sw_na;
+  const uint8_t* act_src;
+  const uint8_t* act_dst;
+  const uint8_t* act_turn;
+  const uint8_t* act_j;
+  const uint8_t* first_other;
+  const uint8_t* port_side;
+  const uint8_t* slot_nroutes;
+  const uint8_t* slot_route_act;
+  const uint8_t* q_w;
+  const int16_t* port_nb;
+  const int16_t* port_len;
+  const int16_t* port_unique;
+  const uint64_t* q_off;
+  const uint32_t* row_base;
+  const int32_t* dist;
+  const int32_t* tr_ed;
+  const int32_t* tr_la;
+  const int32_t* tr_k;
+  const int32_t* tr_target;
+  const int32_t* tr_init_cell;
+  const int32_t* tr_init_dist;
+  const int32_t* tr_init_delay;
+  const uint8_t* tr_init_dir;
+  const int16_t* tr_init_port;
+  const double* eps_tab;
+  const double* lr_tab;
+};
+
+struct SflState {
+  uint32_t E;
+  int32_t* phase;
+  int32_t* elapsed;
+  uint32_t* eflags;
+  int32_t* ep_t;        // learning episodes completed in the current learn() call
+  int32_t* n_test;      // greedy test episodes completed in the current test() call
+  uint32_t* epoch;      // (switch, train) slot epoch
+  uint64_t* rng;        // [5][E]: state hi/lo, inc hi/lo, has<<32|buf
+  uint64_t* seed;       // env seed (reset / malfunction stream)
+  double* cum_reward;
+  int32_t* n_mf;
+  int32_t* ep_dec;
+  int32_t* ep_ticks;
+  int64_t* step_ctr;
+  int64_t* dec_total;
+  uint32_t* masks;      // [4][MAXW][E]: active, arrived, flushed, malfunction-last-tick
+  uint32_t* err;
+  int32_t* tr_pos;      // [T][E] cell index or -1 (off map)
+  uint32_t* tr_bits;    // [T][E] dir | state | prev action | saved action | mf counter | done
+  uint32_t* tr_plan;    // [T][E] packed rail-action queue
+  uint16_t* tr_next;    // [T][E] _train2next_port
+  uint16_t* tr_prev;    // [T][E] _train_prev_port (persists across resets, like the reference)
+  uint16_t* tr_src;     // [T][E] _train_source_port (persists across resets)
+  uint16_t* tr_dec;     // [T][E] switch of the train's queued decision
+  int32_t* tr_delay;    // [T][E] train_to_last_node delay
+  uint16_t* own;        // [T*OWN_MAX][E] ports a train may own (lazily validated)
+  uint8_t* own_n;       // [T][E]
+  int32_t* sc_desired;  // [T][E] tick scratch
+  int32_t* sc_pred;     // [T][E]
+  uint32_t* sc_aux;     // [T][E]
+  uint8_t* occ;         // [H*W][E] occupying train or 0xFF
+  uint8_t* claim;       // [H*W][E] motion-check claim or 0xFF
+  uint64_t* sem;        // [NP][E] semaphore records
+  uint64_t* slot;       // [S*T][E] pending update | reward | epoch
+  uint32_t* counts;     // [S][E] agent_num_interactions
+  double* q;            // [E][q_per_env]
+  uint32_t* touched;    // [E][touched_words] Q-table key set
+};
+
+struct SflCtl {
+  int32_t mode;          // 0 = learn, 1 = greedy test
+  int32_t exploit_freq;  // learn: greedy round before episode t when (t+1) % f == 0
+  int32_t ep_target;     // stop once this many episodes of the mode are done (-1: unlimited)
+  int32_t stats_cap;     // rows in the stats buffers (episode index modulo cap)
+  int64_t dec_budget;    // decisions per env in this launch (<= 0: unlimited)
+  double* st_cum;        // [cap][E]
+  int32_t* st_arrived;   // [cap][E]
+  int32_t* st_mf;        // [cap][E]
+  int32_t* st_dec;       // [cap][E]
+  int32_t* st_ticks;     // [cap][E]
+  int32_t* st_delays;    // [cap][T][E]
+  double* sx_cum;        // exploit rounds [cap][E]
+  int32_t* sx_arrived;   // [cap][E]
+  uint64_t* launch_dec;  // [E] decisions made in this launch
+  uint64_t* launch_ticks;  // [E]
+  uint64_t* launch_bytes;  // [E] algorithmic bytes (SURVEY.md §8(d) model) of this launch
+  uint64_t* trace;       // optional per-decision trace of one env: [trace_cap][4]
+  uint64_t* trace_n;     // records written
+  int32_t trace_env;
+  int32_t trace_cap;
+};
+
+// ---------------------------------------------------------------------------
+// small helpers
+// ---------------------------------------------------------------------------
+SFL_FN int popc32(uint32_t x) { return __builtin_popcount(x); }
+SFL_FN int ctz32(uint32_t x) { return __builtin_ctz(x); }
+
+// tr_bits layout
+SFL_FN uint32_t tb_dir(uint32_t b) { return b & 3u; }
+SFL_FN uint32_t tb_state(uint32_t b) { return (b >> 2) & 7u; }
+SFL_FN uint32_t tb_prev(uint32_t b) { return (b >> 5) & 15u; }
+SFL_FN uint32_t tb_saved(uint32_t b) { return (b >> 9) & 15u; }
+SFL_FN uint32_t tb_mf(uint32_t b) { return (b >> 13) & 0xFFu; }
+SFL_FN uint32_t tb_done(uint32_t b) { return (b >> 21) & 1u; }
+SFL_FN uint32_t tb_make(uint32_t dir, uint32_t state, uint32_t prev, uint32_t saved, uint32_t mf, uint32_t done) {
+  return (dir & 3u) | ((state & 7u) << 2) | ((prev & 15u) << 5) | ((saved & 15u) << 9) | ((mf & 0xFFu) << 13) |
+         ((done & 1u) << 21);
+}
+
+// packed plan: bits 0-3 length, action k in bits 4+4k
+SFL_FN uint32_t pl_len(uint32_t p) { return p & 15u; }
+SFL_FN uint32_t pl_front(uint32_t p) { return (p >> 4) & 15u; }
+SFL_FN uint32_t pl_pop(uint32_t p) { return ((p >> 8) << 4) | (pl_len(p) - 1u); }
+SFL_FN uint32_t pl_push_front(uint32_t p, uint32_t a, uint32_t& err) {
+  uint32_t n = pl_len(p);
+  if (n >= 7u) { err |= E_PLAN_OVF; return p; }
+  return (((p >> 4) << 8) | (a << 4)) | (n + 1u);
+}
+SFL_FN uint32_t pl_push_back(uint32_t p, uint32_t a, uint32_t& err) {
+  uint32_t n = pl_len(p);
+  if (n >= 7u) { err |= E_PLAN_OVF; return p; }
+  return (p & ~15u) | (a << (4u + 4u * n)) | (n + 1u);
+}
+SFL_FN uint32_t pl_at(uint32_t p, uint32_t i) { return (p >> (4u + 4u * i)) & 15u; }
+
+// semaphore record: t0 16 | t1 16 | owner 8 | in 1 | present 1
+SFL_FN uint64_t sem_pack(uint32_t owner, uint32_t is_in, int32_t t0, int32_t t1) {
+  return (uint64_t)(uint16_t)(int16_t)t0 | ((uint64_t)(uint16_t)(int16_t)t1 << 16) | ((uint64_t)(owner & 0xFFu) << 32) |
+         ((uint64_t)(is_in & 1u) << 40) | (1ull << 41);
+}
+SFL_FN bool sem_present(uint64_t r) { return (r >> 41) & 1ull; }
+SFL_FN int32_t sem_t0(uint64_t r) { return (int32_t)(int16_t)(uint16_t)(r & 0xFFFFull); }
+SFL_FN int32_t sem_t1(uint64_t r) { return (int32_t)(int16_t)(uint16_t)((r >> 16) & 0xFFFFull); }
+SFL_FN uint32_t sem_owner(uint64_t r) { return (uint32_t)((r >> 32) & 0xFFull); }
+SFL_FN uint32_t sem_in(uint64_t r) { return (uint32_t)((r >> 40) & 1ull); }
+SFL_FN uint64_t sem_retime(uint64_t r, uint32_t owner, int32_t t0, int32_t t1) {
+  return sem_pack(owner, sem_in(r), t0, t1);
+}
+
+// (switch, train) slot: pending 32 | reward 24 (signed) | epoch 8
+SFL_FN uint32_t slot_pend(uint64_t v, uint32_t epoch) { return ((uint32_t)(v >> 56) == (epoch & 0xFFu)) ? (uint32_t)v : PEND_NONE; }
+SFL_FN int32_t slot_rew(uint64_t v, uint32_t epoch) {
+  if ((uint32_t)(v >> 56) != (epoch & 0xFFu)) return 0;
+  int32_t r = (int32_t)((v >> 32) & 0xFFFFFFull);
+  return (r << 8) >> 8;
+}
+SFL_FN uint64_t slot_make(uint32_t pend, int32_t rew, uint32_t epoch) {
+  return (uint64_t)pend | ((uint64_t)((uint32_t)rew & 0xFFFFFFu) << 32) | ((uint64_t)(epoch & 0xFFu) << 56);
+}
+// pending: switch 12 | slot 2 | state 14 | j 2 (+ all-ones = none)
+SFL_FN uint32_t pend_make(uint32_t s, uint32_t slot, uint32_t state, uint32_t j) {
+  return (s & 0xFFFu) | ((slot & 3u) << 12) | ((state & 0x3FFFu) << 14) | ((j & 3u) << 28);
+}
+
+SFL_FN bool is_moving_action(uint32_t a) { return a == A_LEFT || a == A_FWD || a == A_RIGHT; }
+SFL_FN bool on_map_state(uint32_t s) { return s == S_MOVING || s == S_STOPPED || s == S_MALF; }
+SFL_FN bool off_map_state(uint32_t s) { return s == S_WAITING || s == S_READY || s == S_MF_OFF; }
+
+// ---------------------------------------------------------------------------
+// environment view
+// ---------------------------------------------------------------------------
+struct Env {
+  const SflMap& m;
+  const SflState& s;
+  const uint32_t e;
+  const uint32_t E;
+  uint32_t err;
+  int32_t now;      // rail_env._elapsed_steps
+  uint32_t flags;
+  uint32_t epoch;
+
+  SFL_FN Env(const SflMap& m_, const SflState& s_, uint32_t e_) : m(m_), s(s_), e(e_), E(s_.E), err(0), now(0), flags(0), epoch(0) {}
+  SFL_FN size_t ix(size_t i) const { return i * (size_t)E + e; }
+
+  // grid -----------------------------------------------------------------
+  SFL_FN uint32_t exits(int cell, int d) const { return ((uint32_t)m.grid[cell] >> ((3 - d) * 4)) & 15u; }
+  SFL_FN int move_cell(int cell, int d) const {
+    int r = cell / m.W, c = cell - r * m.W;
+    r += (d == 2) - (d == 0);
+    c += (d == 1) - (d == 3);
+    if (r < 0 || r >= m.H || c < 0 || c >= m.W) return -1;
+    return r * m.W + c;
+  }
+  struct Move {
+    int cell;
+    int dir;
+    bool valid;    // transition_valid
+    bool cell_ok;  // new_cell_valid
+  };
+  // flatland-lite check_action_on_agent
+  SFL_FN Move check_action(uint32_t a, int cell, int dir) const {
+    uint32_t nib = exits(cell, dir);
+    int n = popc32(nib);
+    int nd = dir;
+    int valid = -1;
+    if (a == A_LEFT) {
+      nd = dir + 3;
+      if (n <= 1) valid = 0;
+    } else if (a == A_RIGHT) {
+      nd = dir + 1;
+      if (n <= 1) valid = 0;
+    }
+    nd &= 3;
+    if (a == A_FWD && n == 1) {
+      nd = 3 - (31 - __builtin_clz(nib));
+      valid = 1;
+    }
+    Move mv;
+    mv.cell = move_cell(cell, nd);
+    mv.dir = nd;
+    mv.cell_ok = mv.cell >= 0 && m.grid[mv.cell] != 0;
+    mv.valid = valid < 0 ? (((nib >> (3 - nd)) & 1u) != 0) : (valid != 0);
+    return mv;
+  }
+  SFL_FN bool action_ok(uint32_t a, int cell, int dir) const {
+    Move mv = check_action(a, cell, dir);
+    return mv.cell_ok && mv.valid;
+  }
+  SFL_FN int32_t dist(int h, int cell, int dir) {
+    if (cell < 0) { err |= E_INF_DIST; return 0; }
+    int32_t d = m.dist[(((size_t)m.tr_k[h] * m.H * m.W) + (size_t)cell) * 4 + dir];
+    if (d >= DIST_INF) err |= E_INF_DIST;
+    return d;
+  }
+
+  // train fields -------------------------------------------------------------
+  SFL_FN uint32_t& bits(int h) const { return s.tr_bits[ix(h)]; }
+  SFL_FN int32_t& pos(int h) const { return s.tr_pos[ix(h)]; }
+  SFL_FN uint32_t& plan(int h) const { return s.tr_plan[ix(h)]; }
+  SFL_FN uint16_t& next_port(int h) const { return s.tr_next[ix(h)]; }
+  SFL_FN uint16_t& prev_port(int h) const { return s.tr_prev[ix(h)]; }
+  SFL_FN uint16_t& src_port(int h) const { return s.tr_src[ix(h)]; }
+  SFL_FN uint32_t state_of(int h) const { return tb_state(s.tr_bits[ix(h)]); }
+  SFL_FN uint32_t& mask(int kind, int w) const { return s.masks[((size_t)kind * MAXW + w) * E + e]; }
+
+  // semaphores ---------------------------------------------------------------
+  SFL_FN uint64_t& sem(int p) const { return s.sem[ix(p)]; }
+  SFL_FN void own_add(int h, int p) {
+    if (flags & F_OWN_SCAN) return;
+    uint8_t& n = s.own_n[ix(h)];
+    uint32_t cnt = n;
+    for (uint32_t k = 0; k < cnt; ++k)
+      if (s.own[ix((size_t)h * OWN_MAX + k)] == (uint16_t)p) return;
+    if (cnt == OWN_MAX) {  // compact: drop entries the train no longer owns
+      uint32_t w = 0;
+      for (uint32_t k = 0; k < cnt; ++k) {
+        uint16_t q = s.own[ix((size_t)h * OWN_MAX + k)];
+        uint64_t r = sem(q);
+        if (sem_present(r) && sem_owner(r) == (uint32_t)h) s.own[ix((size_t)h * OWN_MAX + w++)] = q;
+      }
+      cnt = w;
+      if (cnt == OWN_MAX) {  // still full: fall back to full scans for this env
+        flags |= F_OWN_SCAN;
+        return;
+      }
+    }
+    s.own[ix((size_t)h * OWN_MAX + cnt)] = (uint16_t)p;
+    n = (uint8_t)(cnt + 1);
+  }
+  SFL_FN void sem_set(int p, uint64_t rec) {
+    sem(p) = rec;
+    own_add((int)sem_owner(rec), p);
+  }
+  // set if absent, else (io == ovr_io or t0 in the future) -> retime in place (io kept)
+  SFL_FN void sem_put_keep(int p, int h, uint32_t is_in, int32_t span, uint32_t ovr_in) {
+    uint64_t r = sem(p);
+    if (!sem_present(r)) sem_set(p, sem_pack(h, is_in, now, now + span));
+    else if (sem_in(r) == ovr_in || sem_t0(r) > now) sem_set(p, sem_retime(r, h, now, now + span));
+  }
+  // set if absent, else (ovr_in matches or t0 in the future) -> replace whole record
+  SFL_FN void sem_put_replace(int p, int h, uint32_t is_in, int32_t span, int ovr_in) {
+    uint64_t r = sem(p);
+    if (!sem_present(r)) sem_set(p, sem_pack(h, is_in, now, now + span));
+    else if ((ovr_in >= 0 && sem_in(r) == (uint32_t)ovr_in) || sem_t0(r) > now)
+      sem_set(p, sem_pack(h, is_in, now, now + span));
+  }
+  SFL_FN void free_switch_ports(int sw, int h) {
+    const int np = m.sw_np[sw];
+    for (int j = 0; j < np; ++j) {
+      uint64_t r = sem(4 * sw + j);
+      if (sem_present(r) && sem_owner(r) == (uint32_t)h) sem(4 * sw + j) = 0;
+    }
+  }
+  // delete every semaphore owned by h (switch_env.py:370-376)
+  SFL_FN void purge_train(int h) {
+    if (flags & F_OWN_SCAN) {
+      for (int p = 0; p < m.NP; ++p) {
+        uint64_t r = sem(p);
+        if (sem_present(r) && sem_owner(r) == (uint32_t)h) sem(p) = 0;
+      }
+      return;
+    }
+    uint8_t& n = s.own_n[ix(h)];
+    for (uint32_t k = 0; k < n; ++k) {
+      uint16_t p = s.own[ix((size_t)h * OWN_MAX + k)];
+      uint64_t r = sem(p);
+      if (sem_present(r) && sem_owner(r) == (uint32_t)h) sem(p) = 0;
+    }
+    n = 0;
+  }
+  // extend_semaphores for one stopped/malfunctioning train (rail_network.py:233-238)
+  SFL_FN void extend_train(int h) {
+    if (flags & F_OWN_SCAN) {
+      for (int p = 0; p < m.NP; ++p) {
+        uint64_t r = sem(p);
+        if (sem_present(r) && sem_owner(r) == (uint32_t)h) sem(p) = sem_retime(r, h, now, now + (sem_t1(r) - sem_t0(r)));
+      }
+      return;
+    }
+    const uint32_t n = s.own_n[ix(h)];
+    for (uint32_t k = 0; k < n; ++k) {
+      uint16_t p = s.own[ix((size_t)h * OWN_MAX + k)];
+      uint64_t r = sem(p);
+      if (sem_present(r) && sem_owner(r) == (uint32_t)h) sem(p) = sem_retime(r, h, now, now + (sem_t1(r) - sem_t0(r)));
+    }
+  }
+  // observer.py:44-151 (a record's dir field always equals map_direction(port))
+  SFL_FN bool port_blocked(int next_p, int out_p, int h) const {
+    uint64_t r = sem(next_p);
+    if (sem_present(r) && sem_owner(r) != (uint32_t)h && sem_t0(r) <= now && now <= sem_t1(r)) {
+      if (!sem_in(r)) return true;
+      if (state_of((int)sem_owner(r)) == S_MALF) return true;
+    }
+    r = sem(out_p);
+    if (sem_present(r) && sem_owner(r) != (uint32_t)h && sem_t0(r) <= now && now <= sem_t1(r)) {
+      if (sem_in(r)) return true;
+      if (state_of((int)sem_owner(r)) == S_MALF) return true;
+    }
+    return false;
+  }
+
+  // Q-table --------------------------------------------------------------------
+  SFL_FN double* qrow(int sw, int slot, uint32_t state) const {
+    const int g = 4 * sw + slot;
+    return s.q + (size_t)e * m.q_per_env + m.q_off[g] + (size_t)state * m.q_w[g];
+  }
+  SFL_FN void touch(int sw, int slot, uint32_t state) const {
+    const uint32_t row = m.row_base[4 * sw + slot] + state;
+    s.touched[(size_t)e * m.touched_words + (row >> 5)] |= 1u << (row & 31u);
+  }
+  SFL_FN double eps_of(uint32_t n) const { return n < (uint32_t)m.ntab ? m.eps_tab[n] : m.eps0 * pow(m.eps_decay, (double)n); }
+  SFL_FN double lr_of(uint32_t n) const { return n < (uint32_t)m.ntab ? m.lr_tab[n] : m.lr0 * pow(m.lr_decay, (double)n); }
+
+  // rng ------------------------------------------------------------------------
+  SFL_FN Pcg64 rng_load() const {
+    Pcg64 g;
+    g.shi = s.rng[ix(0)];
+    g.slo = s.rng[ix(1)];
+    g.ihi = s.rng[ix(2)];
+    g.ilo = s.rng[ix(3)];
+    uint64_t hb = s.rng[ix(4)];
+    g.has = (uint32_t)(hb >> 32);
+    g.buf = (uint32_t)hb;
+    return g;
+  }
+  SFL_FN void rng_store(const Pcg64& g) const {
+    s.rng[ix(0)] = g.shi;
+    s.rng[ix(1)] = g.slo;
+    s.rng[ix(4)] = ((uint64_t)g.has << 32) | g.buf;
+  }
+};
+
+// ---------------------------------------------------------------------------
+// episode reset (switch_env.py:93-158, _init_ports 507-568)
+// ---------------------------------------------------------------------------
+SFL_FN void env_reset(Env& v) {
+  const SflMap& m = v.m;
+  const SflState& s = v.s;
+  v.now = 0;
+  for (int h = 0; h < m.T; ++h) {
+    int32_t p = v.pos(h);
+    if (p >= 0 && s.occ[v.ix(p)] == (uint8_t)h) s.occ[v.ix(p)] = 0xFF;
+    v.pos(h) = -1;
+    v.bits(h) = tb_make(m.tr_init_dir[h], S_WAITING, A_NONE, 0, 0, 0);
+    v.plan(h) = 0;
+    v.next_port(h) = (uint16_t)m.tr_init_port[h];
+    s.tr_delay[v.ix(h)] = m.tr_init_delay[h];
+    s.own_n[v.ix(h)] = 0;
+  }
+  for (int p = 0; p < m.NP; ++p) v.sem(p) = 0;
+  v.flags &= ~(F_TERM | F_TRUNC | F_OWN_SCAN | F_INFLIGHT);
+  for (int h = 0; h < m.T; ++h) {
+    const int p = m.tr_init_port[h];
+    v.sem_set(p, sem_pack(h, 1, m.tr_ed[h] - 2, m.tr_ed[h] + m.tr_init_dist[h]));
+  }
+  for (int k = 0; k < 4; ++k)
+    for (int w = 0; w < MAXW; ++w) v.mask(k, w) = 0;
+  // new (switch, train) epoch: slots from older episodes read as empty
+  v.epoch = (v.epoch + 1u) & 0xFFu;
+  if (v.epoch == 0) {
+    for (int i = 0; i < m.S * m.T; ++i) s.slot[v.ix(i)] = slot_make(PEND_NONE, 0, 0);
+    v.epoch = 1;
+  }
+  s.cum_reward[v.e] = 0.0;
+  s.n_mf[v.e] = 0;
+  s.ep_dec[v.e] = 0;
+  s.ep_ticks[v.e] = 0;
+  s.step_ctr[v.e] = 0;
+}
+
+// ---------------------------------------------------------------------------
+// one Flatland tick + switchfl bookkeeping + _check_active_switch
+// (switch_env.py:296-401, 427-485; flatland_lite.RailEnv.step)
+// ---------------------------------------------------------------------------
+// sc_aux layout: pa 0-3 | ddir 4-5 | mover 6 | allowed 7 | given 8-11 | has_pred 12 | pred_valid 13
+SFL_FN void env_tick(Env& v) {
+  const SflMap& m = v.m;
+  const SflState& s = v.s;
+  const int32_t t = ++v.now;
+  const uint64_t seed = s.seed[v.e];
+  uint32_t movers[MAXW] = {0, 0, 0, 0};
+
+  // pass 1: plan pop + prediction (switch_env.py:304-339), malfunction draw, action
+  // preprocessing, desired move, cell claims (flatland step, first agent loop)
+  for (int h = 0; h < m.T; ++h) {
+    uint32_t b = v.bits(h);
+    const int32_t pos = v.pos(h);
+    uint32_t st = tb_state(b), dir = tb_dir(b), prev = tb_prev(b), saved = tb_saved(b), mf = tb_mf(b);
+    uint32_t aux = 0;
+    uint32_t given = A_NOTHING;
+    int32_t pred = pos;
+    if (!tb_done(b)) {
+      uint32_t p = v.plan(h);
+      if (pl_len(p) == 0) {
+        given = A_FWD;
+      } else {
+        given = pl_front(p);
+        prev = given;
+        v.plan(h) = pl_pop(p);
+      }
+      if (pos >= 0) {
+        Env::Move mv = v.check_action(given, pos, (int)dir);
+        aux |= 1u << 12;
+        if (mv.valid) {
+          aux |= 1u << 13;
+          pred = mv.cell;
+        }
+      }
+    }
+    if (st != S_DONE && mf == 0 && m.mf_rate > 0.0) {
+      uint64_t z = mf_draw(seed, (uint64_t)t, (uint64_t)h);
+      double u = (double)(z >> 11) * (1.0 / 9007199254740992.0);
+      if (u < m.mf_rate) mf = (uint32_t)(m.mf_min + (int32_t)(mix64(z ^ 0xA0761D6478BD642Full) % (uint64_t)(m.mf_max - m.mf_min + 1))) + 1u;
+    }
+    // preprocess_action
+    uint32_t pa = given;
+    if (pa == A_NOTHING && st == S_MOVING) pa = A_FWD;
+    if (st == S_WAITING) pa = A_NOTHING;
+    const int pc = pos >= 0 ? pos : m.tr_init_cell[h];
+    const int pd = pos >= 0 ? (int)dir : (int)m.tr_init_dir[h];
+    if ((pa == A_LEFT || pa == A_RIGHT) && !v.action_ok(pa, pc, pd)) pa = A_FWD;
+    if (is_moving_action(pa) && !v.action_ok(pa, pc, pd)) pa = A_STOP;
+    if (is_moving_action(pa) && saved == 0 && st != S_DONE) saved = pa;
+    const bool update_allowed = (mf == 0) && pa != A_STOP;
+    int32_t desired = pos;
+    uint32_t ddir = dir;
+    bool mover = false;
+    if (st == S_DONE) {
+    } else if (pos < 0 && saved != 0) {
+      desired = m.tr_init_cell[h];
+      ddir = m.tr_init_dir[h];
+      mover = true;
+    } else if (saved != 0 && update_allowed) {
+      Env::Move mv = v.check_action(saved, pos, (int)dir);
+      desired = mv.cell;
+      ddir = (uint32_t)mv.dir;
+      pa = saved;
+      mover = desired != pos;
+    }
+    if (mover) {
+      movers[h >> 5] |= 1u << (h & 31);
+      uint8_t& c = s.claim[v.ix(desired)];
+      if (c == 0xFF) c = (uint8_t)h;
+    }
+    aux |= pa | (ddir << 4) | ((mover ? 1u : 0u) << 6) | (given << 8);
+    s.sc_aux[v.ix(h)] = aux;
+    s.sc_desired[v.ix(h)] = desired;
+    s.sc_pred[v.ix(h)] = pred;
+    v.bits(h) = tb_make(dir, st, prev, saved, mf, tb_done(b));
+  }
+
+  // pass 2: motion check, least fixed point (flatland_lite.motion_check)
+  uint32_t allowed[MAXW] = {0, 0, 0, 0};
+  bool changed = true;
+  while (changed) {
+    changed = false;
+    for (int w = 0; w < MAXW; ++w) {
+      uint32_t pend = movers[w] & ~allowed[w];
+      while (pend) {
+        const int h = w * 32 + ctz32(pend);
+        pend &= pend - 1u;
+        const int32_t d = s.sc_desired[v.ix(h)];
+        if (s.claim[v.ix(d)] != (uint8_t)h) continue;
+        const uint8_t j = s.occ[v.ix(d)];
+        if (j == 0xFF || (((movers[j >> 5] & allowed[j >> 5]) >> (j & 31)) & 1u)) {
+          allowed[w] |= 1u << (h & 31);
+          changed = true;
+        }
+      }
+    }
+  }
+
+  // pass 3: state machine + positions (flatland step, second agent loop), then
+  // deviation fix, purge of done trains and departure semaphores (switch_env.py:353-384)
+  const bool episode_over_by_time = t >= m.max_episode_steps;
+  bool all_done = true;
+  for (int h = 0; h < m.T; ++h) {
+    uint32_t b = v.bits(h);
+    const int32_t pos = v.pos(h);
+    const uint32_t aux = s.sc_aux[v.ix(h)];
+    const int32_t desired = s.sc_desired[v.ix(h)];
+    uint32_t st = tb_state(b), dir = tb_dir(b), saved = tb_saved(b), mf = tb_mf(b);
+    const uint32_t pa = aux & 15u;
+    const bool mover = (aux >> 6) & 1u;
+    if (mover && s.claim[v.ix(desired)] == (uint8_t)h) s.claim[v.ix(desired)] = 0xFF;
+    const bool in_mf = mf > 0;
+    bool ma = in_mf ? false : (mover && ((allowed[h >> 5] >> (h & 31)) & 1u));
+    const bool valid_move = is_moving_action(pa) && ma;
+    const bool ed_reached = t >= m.tr_ed[h];
+    const uint32_t prev_st = st;
+    switch (st) {
+      case S_WAITING: st = in_mf ? S_MF_OFF : (ed_reached ? S_READY : S_WAITING); break;
+      case S_READY: st = in_mf ? S_MF_OFF : (valid_move ? S_MOVING : S_READY); break;
+      case S_MF_OFF: st = (mf == 0) ? (ed_reached ? S_READY : S_WAITING) : S_MF_OFF; break;
+      case S_MOVING:
+        if (in_mf) st = S_MALF;
+        else if (pa == A_STOP) st = S_STOPPED;
+        else if (pos >= 0 && pos == m.tr_target[h]) st = S_DONE;
+        else if (!ma) st = S_STOPPED;
+        break;
+      case S_STOPPED: st = in_mf ? S_MALF : (valid_move ? S_MOVING : S_STOPPED); break;
+      case S_MALF: st = (mf == 0) ? (valid_move ? S_MOVING : S_STOPPED) : S_MALF; break;
+      default: break;
+    }
+    ma = ma && st != S_DONE;
+    int32_t npos = pos;
+    if (on_map_state(st)) {
+      if (off_map_state(prev_st)) {
+        npos = m.tr_init_cell[h];
+        dir = m.tr_init_dir[h];
+      } else if (ma) {
+        npos = desired;
+        dir = (aux >> 4) & 3u;
+        if (npos == m.tr_target[h]) st = S_DONE;
+      }
+    }
+    const int wi = h >> 5;
+    const uint32_t bit = 1u << (h & 31);
+    if (st == S_DONE && !(v.mask(1, wi) & bit)) {
+      v.mask(1, wi) |= bit;  // arrived (position None, arrival_time set)
+      npos = -1;
+    }
+    if (npos != pos) {
+      if (pos >= 0 && s.occ[v.ix(pos)] == (uint8_t)h) s.occ[v.ix(pos)] = 0xFF;
+      if (npos >= 0) s.occ[v.ix(npos)] = (uint8_t)h;
+    }
+    if (mf > 0) mf -= 1;
+    if (npos >= 0) saved = 0;
+    const bool done = (st == S_DONE) || episode_over_by_time;
+    all_done = all_done && st == S_DONE;
+    v.pos(h) = npos;
+    // switchfl: deviation fix
+    if ((aux >> 12) & 1u) {
+      const int32_t exp = s.sc_pred[v.ix(h)];
+      const uint32_t given = (aux >> 8) & 15u;
+      if (exp != npos && ((aux >> 13) & 1u) && given != A_STOP) {
+        v.plan(h) = pl_push_front(v.plan(h), given, v.err);
+        if (m.cell_sw[exp] >= 0) v.next_port(h) = v.src_port(h);
+      }
+    }
+    if (done) v.purge_train(h);
+    if (t == m.tr_ed[h] - 2) {
+      const int p = v.next_port(h);
+      v.sem_set(p, sem_pack(h, 1, m.tr_ed[h] - 2, m.tr_ed[h] + m.tr_init_dist[h]));
+    }
+    v.bits(h) = tb_make(dir, st, tb_prev(b), saved, mf, done ? 1u : 0u);
+  }
+
+  // pass 4: extend_semaphores (rail_network.py:229-244), malfunction count
+  // (switch_env.py:399-401), _check_active_switch (switch_env.py:427-485)
+  const bool terminated = all_done || episode_over_by_time;
+  int32_t new_mf = 0;
+  for (int h = 0; h < m.T; ++h) {
+    const uint32_t b = v.bits(h);
+    const uint32_t st = tb_state(b);
+    if (st == S_STOPPED || st == S_MALF) v.extend_train(h);
+    if (st == S_MALF) {
+      const int p = v.next_port(h);
+      if (!sem_present(v.sem(p))) v.sem_set(p, sem_pack(h, 1, t, t + m.tr_init_dist[h]));
+    }
+    const int wi = h >> 5;
+    const uint32_t bit = 1u << (h & 31);
+    if (tb_mf(b) > 0) {
+      if (!(v.mask(3, wi) & bit)) new_mf++;
+      v.mask(3, wi) |= bit;
+    } else {
+      v.mask(3, wi) &= ~bit;
+    }
+    const int32_t pos = v.pos(h);
+    if (pos < 0 || st == S_WAITING) continue;
+    const uint32_t p = v.plan(h);
+    const uint32_t nxt = pl_len(p) ? pl_front(p) : A_FWD;
+    Env::Move mv = v.check_action(nxt, pos, (int)tb_dir(b));
+    if (mv.cell < 0) continue;
+    const int sw_at = m.cell_sw[mv.cell];
+    if (sw_at < 0) continue;
+    int sw;
+    if (st == S_READY || st == S_MOVING) sw = sw_at;
+    else if ((st == S_STOPPED || st == S_MALF) && tb_prev(b) == A_STOP) sw = sw_at;
+    else if (st == S_STOPPED || st == S_MALF) sw = v.next_port(h) >> 2;
+    else continue;
+    v.mask(0, wi) |= bit;
+    s.tr_dec[v.ix(h)] = (uint16_t)sw;
+  }
+  s.n_mf[v.e] += new_mf;
+  s.ep_ticks[v.e] += 1;
+  if (terminated) v.flags |= F_TERM;
+}
+
+SFL_FN bool queue_empty(const Env& v) {
+  for (int w = 0; w < MAXW; ++w)
+    if (v.mask(0, w)) return false;
+  return true;
+}
+
+// ---------------------------------------------------------------------------
+// decision: observe (observer.py:246-308), epsilon-greedy (distr_q.py:312-319),
+// _apply_action (switch_env.py:203-294)
+// ---------------------------------------------------------------------------
+struct Decision {
+  int32_t sw, h, slot;
+  uint32_t state;
+  int32_t action, j;
+  int32_t reward;
+  int32_t next_sw;
+};
+
+// value of full-row action a (the full row is default_q except the compact entries)
+SFL_FN double row_val(const Env& v, int sw, int slot, const double* row, int a) {
+  const SflMap& m = v.m;
+  const int na = m.sw_na[sw];
+  if (a == na - 1) return row[m.q_w[4 * sw + slot] - 1];
+  if (m.act_src[sw * 8 + a] == (uint8_t)slot) return row[m.act_j[sw * 8 + a]];
+  return m.default_q;
+}
+
+// np.argmax over the full row, falling back to the first allowed maximum (distr_q.py:468-490)
+SFL_FN int max_action(const Env& v, int sw, int slot, const double* row, const uint32_t amask) {
+  const int na = v.m.sw_na[sw];
+  int best = 0;
+  double mx = row_val(v, sw, slot, row, 0);
+  for (int a = 1; a < na; ++a) {
+    const double val = row_val(v, sw, slot, row, a);
+    if (val > mx) {
+      mx = val;
+      best = a;
+    }
+  }
+  if ((amask >> best) & 1u) return best;
+  int arg = -1;
+  double amx = 0.0;
+  for (int a = 0; a < na; ++a) {
+    if (!((amask >> a) & 1u)) continue;
+    const double val = row_val(v, sw, slot, row, a);
+    if (arg < 0 || val > amx) {
+      arg = a;
+      amx = val;
+    }
+  }
+  return arg;
+}
+
+// max(row) over the full, unmasked row (distr_q.py:449-466)
+SFL_FN double row_max(const Env& v, int sw, int slot, const double* row) {
+  const int na = v.m.sw_na[sw];
+  double mx = row_val(v, sw, slot, row, 0);
+  for (int a = 1; a < na; ++a) {
+    const double val = row_val(v, sw, slot, row, a);
+    mx = val > mx ? val : mx;
+  }
+  return mx;
+}
+
+// rail_network.py:246-278 + 303-416
+SFL_FN int transition_train(Env& v, int h, int in_p, int out_p) {
+  const SflMap& m = v.m;
+  const int target = m.port_nb[out_p];
+  if (v.state_of(h) != S_MALF) {
+    v.free_switch_ports(v.next_port(h) >> 2, h);
+    const uint16_t pp = v.prev_port(h);
+    if (pp != PORT_NONE) v.free_switch_ports(pp >> 2, h);
+  }
+  const int32_t d_ot = m.port_len[out_p];
+  v.sem_put_keep(out_p, h, 0, 3, 0);
+  v.sem_put_keep(target, h, 1, d_ot + 1, 1);
+  const int u = m.port_unique[target];
+  if (u >= 0) {
+    if (u != in_p && u != out_p && u != target) v.sem_put_replace(u, h, 0, d_ot + 1, 0);
+    v.sem_put_replace(u, h, 0, d_ot, -1);
+    const int far = m.port_nb[u];
+    if (far != in_p && far != out_p && far != u) v.sem_put_replace(far, h, 1, d_ot + m.port_len[u] + 1, 1);
+  }
+  if (target != in_p && target != out_p) v.sem_put_replace(target, h, 0, d_ot + 1, 0);
+  v.src_port(h) = (uint16_t)in_p;
+  v.next_port(h) = (uint16_t)target;
+  v.prev_port(h) = (uint16_t)out_p;
+  return target >> 2;
+}
+
+SFL_FN void env_decide(Env& v, Decision& d, bool greedy) {
+  const SflMap& m = v.m;
+  const SflState& s = v.s;
+  // agent_iter: lowest queued train (switch_env.py:418-421, 616-622)
+  int h = 0;
+  for (int w = 0; w < MAXW; ++w) {
+    uint32_t mk = v.mask(0, w);
+    if (mk) {
+      h = w * 32 + ctz32(mk);
+      v.mask(0, w) = mk & (mk - 1u);
+      break;
+    }
+  }
+  const int sw = s.tr_dec[v.ix(h)];
+  const int np = m.sw_np[sw];
+  const int na = m.sw_na[sw];
+  const int pin = v.next_port(h);
+  if ((pin >> 2) != sw) v.err |= E_PORT;
+  const int slot = pin & 3;
+  // observe
+  uint32_t free_bits = 0;
+  for (int j = 0; j < np; ++j) {
+    const int p = 4 * sw + j;
+    if (!v.port_blocked(m.port_nb[p], p, h)) free_bits |= 1u << j;
+  }
+  const uint32_t b = v.bits(h);
+  const int32_t pos = v.pos(h);
+  const int32_t delay = v.now - m.tr_la[h] + v.dist(h, pos, (int)tb_dir(b));
+  const int32_t avail = m.tr_la[h] - m.tr_ed[h];
+  const uint32_t lvl = delay <= 0 ? 0u : (delay <= avail * 20 ? 1u : 2u);
+  const uint32_t state = ((free_bits * (uint32_t)m.K) + (uint32_t)m.tr_k[h]) * 3u + lvl;
+  uint32_t amask = 1u << (na - 1);
+  for (int a = 0; a < na - 1; ++a)
+    if (m.act_src[sw * 8 + a] == (uint8_t)slot && ((free_bits >> m.act_dst[sw * 8 + a]) & 1u)) amask |= 1u << a;
+  const int32_t reward = slot_rew(s.slot[v.ix((size_t)sw * m.T + h)], v.epoch);
+
+  // epsilon-greedy
+  int action;
+  const double* row = v.qrow(sw, slot, state);
+  bool explore = false;
+  if (!greedy) {
+    Pcg64 g = v.rng_load();
+    const double eps = v.eps_of(s.counts[v.ix(sw)]);
+    if (pcg_double(g) < eps) {
+      explore = true;
+      const uint32_t sub_seed = pcg_bounded(g, 2147483646u);
+      Pcg64 sub;
+      pcg_from_seedseq(sub_seed, sub);
+      const uint32_t nvalid = (uint32_t)popc32(amask);
+      uint32_t pick = pcg_bounded(sub, nvalid - 1u);
+      uint32_t mk = amask;
+      for (uint32_t k = 0; k < pick; ++k) mk &= mk - 1u;
+      action = ctz32(mk);
+    }
+    v.rng_store(g);
+  }
+  if (!explore) {
+    v.touch(sw, slot, state);
+    action = max_action(v, sw, slot, row, amask);
+  }
+  if (action < 0 || action >= na) v.err |= E_BAD_ACTION;
+
+  // _apply_action
+  const int stop = na - 1;
+  bool moving = false;
+  uint32_t turn = A_FWD;
+  int in_p = pin, out_p = pin;
+  if (action != stop && (pin >> 2) == sw) {
+    const int src = m.act_src[sw * 8 + action];
+    if (src == slot) {
+      moving = true;
+      turn = m.act_turn[sw * 8 + action];
+      in_p = 4 * sw + src;
+      out_p = 4 * sw + m.act_dst[sw * 8 + action];
+    }
+  }
+  int next_sw = sw;
+  int target = -1;
+  if (moving) {
+    next_sw = transition_train(v, h, in_p, out_p);
+    target = m.port_nb[out_p];
+  }
+  uint32_t p = v.plan(h);
+  if (moving && pl_len(p) > 0) {
+    p = (p & 0xF0u) | 1u;  // plan[:1]
+    p = pl_push_back(p, turn, v.err);
+  } else if (!moving) {
+    p = pl_push_front(p, A_STOP, v.err);
+  } else {
+    p = pl_push_back(p, A_FWD, v.err);
+    p = pl_push_back(p, turn, v.err);
+  }
+  v.plan(h) = p;
+  bool all_blocked;
+  if (moving) {
+    all_blocked = v.port_blocked(target, out_p, h);
+  } else {
+    all_blocked = true;
+    for (int a = 0; a < na - 1; ++a) {
+      if (m.act_src[sw * 8 + a] != (uint8_t)slot) continue;
+      const int o = 4 * sw + m.act_dst[sw * 8 + a];
+      if (!v.port_blocked(m.port_nb[o], o, h)) all_blocked = false;
+    }
+  }
+  // reward_func.py:23-78: project the position along the non-STOP plan
+  int pc = pos, pd = (int)tb_dir(b);
+  const uint32_t n = pl_len(p);
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint32_t a = pl_at(p, i);
+    if (a == A_STOP) continue;
+    if (pc < 0) break;
+    Env::Move mv = v.check_action(a, pc, pd);
+    pc = mv.cell;
+    pd = mv.dir;
+  }
+  const int32_t cur = v.now - m.tr_la[h] + v.dist(h, pc, pd);
+  const int32_t diff = s.tr_delay[v.ix(h)] - cur;
+  const int32_t r_new = (pl_front(p) == A_STOP && !all_blocked) ? diff - 1300 : diff;
+  uint64_t& sl = s.slot[v.ix((size_t)next_sw * m.T + h)];
+  sl = slot_make(slot_pend(sl, v.epoch), r_new, v.epoch);
+  s.tr_delay[v.ix(h)] = cur;
+
+  d.sw = sw;
+  d.h = h;
+  d.slot = slot;
+  d.state = state;
+  d.action = action;
+  d.j = (action == stop) ? (m.q_w[4 * sw + slot] - 1) : m.act_j[sw * 8 + action];
+  d.reward = reward;
+  d.next_sw = next_sw;
+}
+
+// post-step part of the learn loop (distr_q.py:322-362)
+SFL_FN void env_post(Env& v, const Decision& d) {
+  const SflMap& m = v.m;
+  const SflState& s = v.s;
+  uint64_t& here = s.slot[v.ix((size_t)d.sw * m.T + d.h)];
+  const uint32_t pend = slot_pend(here, v.epoch);
+  if (pend != PEND_NONE) {
+    const int ps = (int)(pend & 0xFFFu);
+    const int pslot = (int)((pend >> 12) & 3u);
+    const uint32_t pstate = (pend >> 14) & 0x3FFFu;
+    const int pj = (int)((pend >> 28) & 3u);
+    v.touch(ps, pslot, pstate);
+    const double lr = v.lr_of(s.counts[v.ix(ps)]);
+    double* q = v.qrow(ps, pslot, pstate) + pj;
+    const double r = (double)d.reward;
+    if (d.sw != ps) {
+      v.touch(d.sw, d.slot, d.state);
+      const double mq = row_max(v, d.sw, d.slot, v.qrow(d.sw, d.slot, d.state));
+      const double a = (1.0 - lr) * *q;
+      const double bb = lr * (r + m.gamma * mq);
+      *q = a + bb;
+    } else {
+      const double a = (1.0 - lr) * *q;
+      const double bb = lr * r;
+      *q = a + bb;
+    }
+    here = slot_make(PEND_NONE, slot_rew(here, v.epoch), v.epoch);
+  }
+  uint64_t& nxt = s.slot[v.ix((size_t)d.next_sw * m.T + d.h)];
+  nxt = slot_make(pend_make((uint32_t)d.sw, (uint32_t)d.slot, d.state, (uint32_t)d.j), slot_rew(nxt, v.epoch), v.epoch);
+  // destination bonus for newly arrived trains (distr_q.py:344-356)
+  for (int w = 0; w < MAXW; ++w) {
+    uint32_t fresh = v.mask(1, w) & ~v.mask(2, w);
+    if (!fresh) continue;
+    v.mask(2, w) |= fresh;
+    while (fresh) {
+      const int tr = w * 32 + ctz32(fresh);
+      fresh &= fresh - 1u;
+      for (int sw2 = 0; sw2 < m.S; ++sw2) {
+        uint64_t& sl = s.slot[v.ix((size_t)sw2 * m.T + tr)];
+        const uint32_t pe = slot_pend(sl, v.epoch);
+        if (pe == PEND_NONE) continue;
+        const int ps = (int)(pe & 0xFFFu);
+        const int pslot = (int)((pe >> 12) & 3u);
+        const uint32_t pstate = (pe >> 14) & 0x3FFFu;
+        const int pj = (int)((pe >> 28) & 3u);
+        v.touch(ps, pslot, pstate);
+        const double lr = v.lr_of(s.counts[v.ix(ps)]);
+        double* q = v.qrow(ps, pslot, pstate) + pj;
+        const double a = (1.0 - lr) * *q;
+        const double bb = lr * (1000.0 + m.gamma * 0.0);
+        *q = a + bb;
+        sl = slot_make(PEND_NONE, slot_rew(sl, v.epoch), v.epoch);
+      }
+    }
+  }
+  s.counts[v.ix(d.sw)] += 1u;
+}
+
+// order-independent checksum of the semaphore table (trace/debug only)
+SFL_FN uint64_t sem_checksum(const Env& v) {
+  uint64_t c = 0;
+  for (int p = 0; p < v.m.NP; ++p) {
+    const uint64_t r = v.sem(p);
+    if (sem_present(r)) c += mix64(((uint64_t)p << 42) ^ r);
+  }
+  return c;
+}
+
+SFL_FN void trace_decision(const Env& v, const SflCtl& c, const Decision& d) {
+  const uint64_t n = *c.trace_n;
+  if (n < (uint64_t)c.trace_cap) {
+    uint64_t* t = c.trace + 4 * n;
+    t[0] = (uint64_t)(uint32_t)v.now | ((uint64_t)(uint32_t)d.sw << 16) | ((uint64_t)(uint32_t)d.h << 32) |
+           ((uint64_t)(uint32_t)d.action << 48);
+    t[1] = (uint64_t)d.state | ((uint64_t)(uint32_t)d.reward << 32);
+    t[2] = sem_checksum(v);
+    t[3] = (uint64_t)(uint32_t)d.next_sw;
+  }
+  *c.trace_n = n + 1;
+}
+
+// ---------------------------------------------------------------------------
+// driver: one env until its episode target / decision budget
+// ---------------------------------------------------------------------------
+SFL_FN void env_run(const SflMap& m, const SflState& s, const SflCtl& c, uint32_t e) {
+  Env v(m, s, e);
+  v.flags = s.eflags[e];
+  v.now = s.elapsed[e];
+  v.epoch = s.epoch[e];
+  v.err = s.err[e];
+  int32_t phase = s.phase[e];
+  uint64_t dec = 0, ticks = 0, abytes = 0;
+  Decision d;
+  d.sw = d.h = d.slot = d.action = d.j = d.reward = d.next_sw = 0;
+  d.state = 0;
+  double cum = s.cum_reward[e];
+  const bool test_mode = c.mode == 1;
+  while (true) {
+    if (phase == PH_RESET) {
+      // learn: optional greedy round before episode t (distr_q.py:278-281)
+      if (test_mode) {
+        if (c.ep_target >= 0 && s.n_test[e] >= c.ep_target) break;
+        v.flags |= F_GREEDY;
+      } else {
+        if (c.ep_target >= 0 && s.ep_t[e] >= c.ep_target) break;
+        const int32_t t = s.ep_t[e];
+        if (c.exploit_freq > 0 && (t + 1) % c.exploit_freq == 0 && !(v.flags & F_EXPLOIT_DONE)) v.flags |= F_GREEDY;
+        else v.flags &= ~F_GREEDY;
+      }
+      env_reset(v);
+      cum = 0.0;
+      phase = PH_TICK;
+    } else if (phase == PH_TICK) {
+      int live = m.T;
+      for (int w = 0; w < MAXW; ++w) live -= popc32(v.mask(1, w));
+      abytes += 36ull * (uint64_t)live;
+      env_tick(v);
+      ticks++;
+      if (v.flags & F_TERM) phase = (v.flags & F_INFLIGHT) ? PH_POST : PH_END;
+      else if (!queue_empty(v)) phase = (v.flags & F_INFLIGHT) ? PH_POST : PH_DECIDE;
+    } else if (phase == PH_DECIDE) {
+      env_decide(v, d, (v.flags & F_GREEDY) != 0);
+      abytes += 220ull + 48ull * m.sw_np[d.sw] + 8ull * m.sw_na[d.sw];
+      v.flags |= F_INFLIGHT;
+      phase = queue_empty(v) ? PH_TICK : PH_POST;
+    } else if (phase == PH_POST) {
+      if (!(v.flags & F_GREEDY)) env_post(v, d);
+      if (c.trace && (int32_t)e == c.trace_env) trace_decision(v, c, d);
+      v.flags &= ~F_INFLIGHT;
+      cum += (double)d.reward;
+      s.ep_dec[e] += 1;
+      s.dec_total[e] += 1;
+      s.step_ctr[e] += 1;
+      if (s.step_ctr[e] > m.max_steps) v.flags |= F_TRUNC;
+      dec++;
+      phase = (v.flags & (F_TERM | F_TRUNC)) ? PH_END : PH_DECIDE;
+      if (c.dec_budget > 0 && (int64_t)dec >= c.dec_budget) break;
+    } else {  // PH_END
+      int arrived = 0;
+      for (int w = 0; w < MAXW; ++w) arrived += popc32(v.mask(1, w));
+      const size_t cap = (size_t)(c.stats_cap > 0 ? c.stats_cap : 1);
+      if (v.flags & F_GREEDY) {
+        if (test_mode) {
+          const int32_t i = s.n_test[e];
+          if (c.st_cum && c.stats_cap > 0) {
+            const size_t row = (size_t)i % cap;
+            c.st_cum[row * s.E + e] = cum;
+            c.st_arrived[row * s.E + e] = arrived;
+            c.st_mf[row * s.E + e] = s.n_mf[e];
+            c.st_dec[row * s.E + e] = s.ep_dec[e];
+            c.st_ticks[row * s.E + e] = s.ep_ticks[e];
+            for (int h = 0; h < m.T; ++h) c.st_delays[(row * m.T + h) * s.E + e] = s.tr_delay[v.ix(h)];
+          }
+          s.n_test[e] += 1;
+        } else {
+          const int32_t i = s.ep_t[e];
+          if (c.sx_cum && c.stats_cap > 0) {
+            const size_t row = (size_t)i % cap;
+            c.sx_cum[row * s.E + e] = cum;
+            c.sx_arrived[row * s.E + e] = arrived;
+          }
+          v.flags |= F_EXPLOIT_DONE;
+        }
+      } else {
+        const int32_t i = s.ep_t[e];
+        if (c.st_cum && c.stats_cap > 0) {
+          const size_t row = (size_t)i % cap;
+          c.st_cum[row * s.E + e] = cum;
+          c.st_arrived[row * s.E + e] = arrived;
+          c.st_mf[row * s.E + e] = s.n_mf[e];
+          c.st_dec[row * s.E + e] = s.ep_dec[e];
+          c.st_ticks[row * s.E + e] = s.ep_ticks[e];
+          for (int h = 0; h < m.T; ++h) c.st_delays[(row * m.T + h) * s.E + e] = s.tr_delay[v.ix(h)];
+        }
+        s.ep_t[e] += 1;
+        v.flags &= ~F_EXPLOIT_DONE;
+      }
+      phase = PH_RESET;
+    }
+  }
+  s.phase[e] = phase;
+  s.elapsed[e] = v.now;
+  s.eflags[e] = v.flags;
+  s.epoch[e] = v.epoch;
+  s.err[e] = v.err;
+  s.cum_reward[e] = cum;
+  if (c.launch_dec) c.launch_dec[e] = dec;
+  if (c.launch_ticks) c.launch_ticks[e] = ticks;
+  if (c.launch_bytes) c.launch_bytes[e] = abytes;
+}
+
+}  // namespace sfl

@@ -1,0 +1,369 @@
+// Engine: owns one batch of lock-step environments on one device and implements
+// the C-ABI of include/sfl.h.  Templated over a backend (HIP device memory +
+// kernel launches in sfl.hip; host memory + a plain loop in the test-only
+// host build sfl_hostsim.cpp) so both builds share every line above the
+// per-env kernel body.
+#pragma once
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/sfl.h"
+#include "sfl_core.h"
+
+namespace sfl {
+
+static thread_local std::string g_last_error;
+
+inline int fail(const std::string& msg) {
+  g_last_error = msg;
+  return -1;
+}
+
+template <class B>
+struct Handle {
+  B be;
+  SflMap map{};
+  SflState st{};
+  uint32_t E = 0;
+  int device = 0;
+  std::vector<void*> allocs;
+  std::vector<uint64_t> seeds;
+  // host copies of small per-env counters for reporting
+  std::vector<uint64_t> h_dec, h_ticks, h_bytes;
+  uint64_t* d_launch_dec = nullptr;
+  uint64_t* d_launch_ticks = nullptr;
+  uint64_t* d_launch_bytes = nullptr;
+  float last_kernel_ms = 0.f;
+
+  template <class T>
+  T* dalloc(size_t n) {
+    if (n == 0) n = 1;
+    void* p = be.alloc(n * sizeof(T));
+    if (!p) return nullptr;
+    allocs.push_back(p);
+    return (T*)p;
+  }
+  template <class T>
+  const T* upload(const T* src, size_t n) {
+    T* d = dalloc<T>(n);
+    if (d && src && n) be.h2d(d, src, n * sizeof(T));
+    return d;
+  }
+  ~Handle() {
+    for (void* p : allocs) be.free(p);
+  }
+};
+
+template <class B>
+int create(const sfl_map_desc* md, const sfl_hparams* hp, uint32_t n_envs, const uint64_t* env_seeds, int device,
+           Handle<B>** out) {
+  if (!md || !hp || !out || n_envs == 0) return fail("sfl_create: null argument or zero envs");
+  if (md->T > 32 * MAXW) return fail("sfl_create: at most 128 trains per env");
+  if (md->S * 4 >= 0xFFFF) return fail("sfl_create: too many switches");
+  if (md->K < 1 || md->K > 341) return fail("sfl_create: station count out of range");
+  auto* h = new Handle<B>();
+  h->device = device;
+  if (int rc = h->be.init(device)) {
+    delete h;
+    return fail(std::string("sfl_create: backend init failed: ") + h->be.error());
+  }
+  h->E = n_envs;
+  SflMap& m = h->map;
+  const size_t HW = (size_t)md->H * md->W, NP = (size_t)md->S * 4, S = md->S, T = md->T;
+  m.H = md->H;
+  m.W = md->W;
+  m.S = md->S;
+  m.T = md->T;
+  m.K = md->K;
+  m.NP = (int32_t)NP;
+  m.max_episode_steps = md->max_episode_steps;
+  m.mf_rate = md->mf_rate;
+  m.mf_min = md->mf_min;
+  m.mf_max = md->mf_max;
+  m.gamma = hp->gamma;
+  m.eps0 = hp->epsilon;
+  m.eps_decay = hp->epsilon_decay_rate;
+  m.lr0 = hp->lr;
+  m.lr_decay = hp->lr_decay_rate;
+  m.default_q = hp->default_q;
+  m.max_steps = hp->max_steps;
+  m.ntab = hp->ntab;
+  m.q_per_env = md->q_per_env;
+  m.rows_per_env = md->rows_per_env;
+  m.touched_words = (md->rows_per_env + 31u) / 32u;
+  m.grid = h->upload(md->grid, HW);
+  m.cell_sw = h->upload(md->cell_sw, HW);
+  m.sw_np = h->upload(md->sw_np, S);
+  m.sw_na = h->upload(md->sw_na, S);
+  m.act_src = h->upload(md->act_src, S * 8);
+  m.act_dst = h->upload(md->act_dst, S * 8);
+  m.act_turn = h->upload(md->act_turn, S * 8);
+  m.act_j = h->upload(md->act_j, S * 8);
+  m.first_other = h->upload(md->first_other, NP);
+  m.port_side = h->upload(md->port_side, NP);
+  m.slot_nroutes = h->upload(md->slot_nroutes, NP);
+  m.slot_route_act = h->upload(md->slot_route_act, NP * 4);
+  m.q_w = h->upload(md->q_w, NP);
+  m.port_nb = h->upload(md->port_nb, NP);
+  m.port_len = h->upload(md->port_len, NP);
+  m.port_unique = h->upload(md->port_unique, NP);
+  m.q_off = h->upload(md->q_off, NP);
+  m.row_base = h->upload(md->row_base, NP);
+  m.dist = h->upload(md->dist, (size_t)md->K * HW * 4);
+  m.tr_ed = h->upload(md->tr_ed, T);
+  m.tr_la = h->upload(md->tr_la, T);
+  m.tr_k = h->upload(md->tr_k, T);
+  m.tr_target = h->upload(md->tr_target, T);
+  m.tr_init_cell = h->upload(md->tr_init_cell, T);
+  m.tr_init_dist = h->upload(md->tr_init_dist, T);
+  m.tr_init_delay = h->upload(md->tr_init_delay, T);
+  m.tr_init_dir = h->upload(md->tr_init_dir, T);
+  m.tr_init_port = h->upload(md->tr_init_port, T);
+  m.eps_tab = h->upload(hp->eps_tab, (size_t)hp->ntab);
+  m.lr_tab = h->upload(hp->lr_tab, (size_t)hp->ntab);
+
+  SflState& s = h->st;
+  const size_t E = n_envs;
+  s.E = n_envs;
+  s.phase = h->template dalloc<int32_t>(E);
+  s.elapsed = h->template dalloc<int32_t>(E);
+  s.eflags = h->template dalloc<uint32_t>(E);
+  s.ep_t = h->template dalloc<int32_t>(E);
+  s.n_test = h->template dalloc<int32_t>(E);
+  s.epoch = h->template dalloc<uint32_t>(E);
+  s.rng = h->template dalloc<uint64_t>(5 * E);
+  s.seed = h->template dalloc<uint64_t>(E);
+  s.cum_reward = h->template dalloc<double>(E);
+  s.n_mf = h->template dalloc<int32_t>(E);
+  s.ep_dec = h->template dalloc<int32_t>(E);
+  s.ep_ticks = h->template dalloc<int32_t>(E);
+  s.step_ctr = h->template dalloc<int64_t>(E);
+  s.dec_total = h->template dalloc<int64_t>(E);
+  s.masks = h->template dalloc<uint32_t>(4 * MAXW * E);
+  s.err = h->template dalloc<uint32_t>(E);
+  s.tr_pos = h->template dalloc<int32_t>(T * E);
+  s.tr_bits = h->template dalloc<uint32_t>(T * E);
+  s.tr_plan = h->template dalloc<uint32_t>(T * E);
+  s.tr_next = h->template dalloc<uint16_t>(T * E);
+  s.tr_prev = h->template dalloc<uint16_t>(T * E);
+  s.tr_src = h->template dalloc<uint16_t>(T * E);
+  s.tr_dec = h->template dalloc<uint16_t>(T * E);
+  s.tr_delay = h->template dalloc<int32_t>(T * E);
+  s.own = h->template dalloc<uint16_t>(T * OWN_MAX * E);
+  s.own_n = h->template dalloc<uint8_t>(T * E);
+  s.sc_desired = h->template dalloc<int32_t>(T * E);
+  s.sc_pred = h->template dalloc<int32_t>(T * E);
+  s.sc_aux = h->template dalloc<uint32_t>(T * E);
+  s.occ = h->template dalloc<uint8_t>(HW * E);
+  s.claim = h->template dalloc<uint8_t>(HW * E);
+  s.sem = h->template dalloc<uint64_t>(NP * E);
+  s.slot = h->template dalloc<uint64_t>(S * T * E);
+  s.counts = h->template dalloc<uint32_t>(S * E);
+  s.q = h->template dalloc<double>((size_t)m.q_per_env * E);
+  s.touched = h->template dalloc<uint32_t>((size_t)m.touched_words * E);
+  h->d_launch_dec = h->template dalloc<uint64_t>(E);
+  h->d_launch_ticks = h->template dalloc<uint64_t>(E);
+  h->d_launch_bytes = h->template dalloc<uint64_t>(E);
+  for (void* p : h->allocs)
+    if (!p) {
+      delete h;
+      return fail("sfl_create: device allocation failed");
+    }
+  if (!m.grid || !s.q) {
+    delete h;
+    return fail("sfl_create: device allocation failed (out of memory?)");
+  }
+  // initial values
+  h->be.memset(s.phase, 0, E * 4);
+  h->be.memset(s.elapsed, 0, E * 4);
+  h->be.memset(s.eflags, 0, E * 4);
+  h->be.memset(s.ep_t, 0, E * 4);
+  h->be.memset(s.n_test, 0, E * 4);
+  h->be.memset(s.epoch, 0, E * 4);
+  h->be.memset(s.rng, 0, 5 * E * 8);
+  h->be.memset(s.cum_reward, 0, E * 8);
+  h->be.memset(s.n_mf, 0, E * 4);
+  h->be.memset(s.ep_dec, 0, E * 4);
+  h->be.memset(s.ep_ticks, 0, E * 4);
+  h->be.memset(s.step_ctr, 0, E * 8);
+  h->be.memset(s.dec_total, 0, E * 8);
+  h->be.memset(s.masks, 0, 4 * MAXW * E * 4);
+  h->be.memset(s.err, 0, E * 4);
+  h->be.memset(s.tr_pos, 0xFF, T * E * 4);  // -1: off map
+  h->be.memset(s.tr_bits, 0, T * E * 4);
+  h->be.memset(s.tr_plan, 0, T * E * 4);
+  h->be.memset(s.tr_next, 0, T * E * 2);
+  h->be.memset(s.tr_prev, 0xFF, T * E * 2);  // None
+  h->be.memset(s.tr_src, 0xFF, T * E * 2);   // None
+  h->be.memset(s.tr_dec, 0, T * E * 2);
+  h->be.memset(s.tr_delay, 0, T * E * 4);
+  h->be.memset(s.own_n, 0, T * E);
+  h->be.memset(s.occ, 0xFF, HW * E);
+  h->be.memset(s.claim, 0xFF, HW * E);
+  h->be.memset(s.sem, 0, NP * E * 8);
+  h->be.memset(s.slot, 0, S * T * E * 8);
+  h->be.memset(s.counts, 0, S * E * 4);
+  h->be.memset(s.touched, 0, (size_t)m.touched_words * E * 4);
+  h->be.fill_f64(s.q, m.default_q, (size_t)m.q_per_env * E);
+  h->seeds.assign(env_seeds, env_seeds + E);
+  h->be.h2d(s.seed, env_seeds, E * 8);
+  if (int rc = h->be.sync()) {
+    delete h;
+    return fail(std::string("sfl_create: ") + h->be.error());
+  }
+  *out = h;
+  return 0;
+}
+
+// rng_states: [E][5] (state hi, state lo, inc hi, inc lo, has<<32|buf) — numpy's
+// default_rng(seed).bit_generator.state, computed on the host.
+template <class B>
+int learn_begin(Handle<B>* h, const uint64_t* rng_states) {
+  const size_t E = h->E;
+  std::vector<uint64_t> soa(5 * E);
+  for (size_t e = 0; e < E; ++e)
+    for (int k = 0; k < 5; ++k) soa[k * E + e] = rng_states[e * 5 + k];
+  h->be.h2d(h->st.rng, soa.data(), soa.size() * 8);
+  h->be.memset(h->st.counts, 0, (size_t)h->map.S * E * 4);
+  h->be.memset(h->st.ep_t, 0, E * 4);
+  // every env starts the learn() call with a fresh reset, and no exploit round done yet
+  std::vector<int32_t> ph(E, PH_RESET);
+  h->be.h2d(h->st.phase, ph.data(), E * 4);
+  std::vector<uint32_t> fl(E);
+  h->be.d2h(fl.data(), h->st.eflags, E * 4);
+  for (auto& f : fl) f &= ~(F_EXPLOIT_DONE | F_INFLIGHT | F_GREEDY);
+  h->be.h2d(h->st.eflags, fl.data(), E * 4);
+  return h->be.sync() ? fail(h->be.error()) : 0;
+}
+
+template <class B>
+int test_begin(Handle<B>* h) {
+  const size_t E = h->E;
+  h->be.memset(h->st.n_test, 0, E * 4);
+  std::vector<int32_t> ph(E, PH_RESET);
+  h->be.h2d(h->st.phase, ph.data(), E * 4);
+  return h->be.sync() ? fail(h->be.error()) : 0;
+}
+
+template <class B>
+int mark_exploit_done(Handle<B>* h) {
+  const size_t E = h->E;
+  std::vector<uint32_t> fl(E);
+  h->be.d2h(fl.data(), h->st.eflags, E * 4);
+  for (auto& f : fl) f |= F_EXPLOIT_DONE;
+  h->be.h2d(h->st.eflags, fl.data(), E * 4);
+  return h->be.sync() ? fail(h->be.error()) : 0;
+}
+
+// Q-init patch rows (distr_q.py:81-181): the same rows for every env
+template <class B>
+int apply_qinit(Handle<B>* h, uint32_t n_rows, const uint32_t* row_port, const uint32_t* row_state,
+                const double* values /*[n_rows][4], NaN = default_q*/) {
+  if (n_rows == 0) return 0;
+  uint32_t* d_port = h->template dalloc<uint32_t>(n_rows);
+  uint32_t* d_state = h->template dalloc<uint32_t>(n_rows);
+  double* d_vals = h->template dalloc<double>((size_t)n_rows * 4);
+  if (!d_port || !d_state || !d_vals) return fail("sfl_apply_qinit: allocation failed");
+  h->be.h2d(d_port, row_port, n_rows * 4);
+  h->be.h2d(d_state, row_state, n_rows * 4);
+  h->be.h2d(d_vals, values, (size_t)n_rows * 4 * 8);
+  h->be.qinit(h->map, h->st, n_rows, d_port, d_state, d_vals);
+  int rc = h->be.sync();
+  // release the scratch
+  for (int k = 0; k < 3; ++k) {
+    h->be.free(h->allocs.back());
+    h->allocs.pop_back();
+  }
+  return rc ? fail(h->be.error()) : 0;
+}
+
+template <class B>
+int check_errors(Handle<B>* h) {
+  std::vector<uint32_t> err(h->E);
+  h->be.d2h(err.data(), h->st.err, h->E * 4);
+  if (h->be.sync()) return fail(h->be.error());
+  for (uint32_t e = 0; e < h->E; ++e)
+    if (err[e]) {
+      char buf[160];
+      snprintf(buf, sizeof buf, "env %u: error flags 0x%x (1=inf distance, 2=plan overflow, 4=port mismatch, 8=bad action)",
+               e, err[e]);
+      return fail(buf);
+    }
+  return 0;
+}
+
+template <class B>
+int run(Handle<B>* h, const SflCtl& c_in, sfl_run_args* args) {
+  SflCtl c = c_in;
+  const size_t E = h->E, T = h->map.T;
+  const int32_t cap = args ? args->stats_cap : 0;
+  std::vector<void*> scratch;
+  auto scr = [&](size_t bytes) -> void* {
+    void* p = h->be.alloc(bytes ? bytes : 1);
+    scratch.push_back(p);
+    return p;
+  };
+  c.stats_cap = cap;
+  if (args && cap > 0) {
+    c.st_cum = (double*)scr((size_t)cap * E * 8);
+    c.st_arrived = (int32_t*)scr((size_t)cap * E * 4);
+    c.st_mf = (int32_t*)scr((size_t)cap * E * 4);
+    c.st_dec = (int32_t*)scr((size_t)cap * E * 4);
+    c.st_ticks = (int32_t*)scr((size_t)cap * E * 4);
+    c.st_delays = (int32_t*)scr((size_t)cap * T * E * 4);
+    c.sx_cum = (double*)scr((size_t)cap * E * 8);
+    c.sx_arrived = (int32_t*)scr((size_t)cap * E * 4);
+    for (void* p : scratch)
+      if (!p) {
+        for (void* q : scratch) h->be.free(q);
+        return fail("sfl_run: stats allocation failed");
+      }
+    h->be.memset(c.sx_cum, 0, (size_t)cap * E * 8);
+    h->be.memset(c.sx_arrived, 0, (size_t)cap * E * 4);
+  }
+  c.launch_dec = h->d_launch_dec;
+  c.launch_ticks = h->d_launch_ticks;
+  c.launch_bytes = h->d_launch_bytes;
+  uint64_t* d_trace = nullptr;
+  uint64_t* d_trace_n = nullptr;
+  if (args && args->trace && args->trace_cap > 0) {
+    d_trace = (uint64_t*)scr((size_t)args->trace_cap * 32);
+    d_trace_n = (uint64_t*)scr(8);
+    if (!d_trace || !d_trace_n) {
+      for (void* q : scratch) h->be.free(q);
+      return fail("sfl_run: trace allocation failed");
+    }
+    h->be.memset(d_trace_n, 0, 8);
+    c.trace = d_trace;
+    c.trace_n = d_trace_n;
+    c.trace_env = args->trace_env;
+    c.trace_cap = args->trace_cap;
+  }
+  float ms = 0.f;
+  int rc = h->be.run(h->map, h->st, c, &ms);
+  h->last_kernel_ms = ms;
+  if (!rc && args && cap > 0) {
+    if (args->cum_reward) h->be.d2h(args->cum_reward, c.st_cum, (size_t)cap * E * 8);
+    if (args->arrived) h->be.d2h(args->arrived, c.st_arrived, (size_t)cap * E * 4);
+    if (args->malfunctions) h->be.d2h(args->malfunctions, c.st_mf, (size_t)cap * E * 4);
+    if (args->decisions) h->be.d2h(args->decisions, c.st_dec, (size_t)cap * E * 4);
+    if (args->ticks) h->be.d2h(args->ticks, c.st_ticks, (size_t)cap * E * 4);
+    if (args->delays) h->be.d2h(args->delays, c.st_delays, (size_t)cap * T * E * 4);
+    if (args->exploit_cum) h->be.d2h(args->exploit_cum, c.sx_cum, (size_t)cap * E * 8);
+    if (args->exploit_arrived) h->be.d2h(args->exploit_arrived, c.sx_arrived, (size_t)cap * E * 4);
+  }
+  if (!rc && d_trace) {
+    h->be.d2h(args->trace_n, d_trace_n, 8);
+    h->be.d2h(args->trace, d_trace, (size_t)args->trace_cap * 32);
+  }
+  if (!rc) rc = h->be.sync();
+  for (void* p : scratch) h->be.free(p);
+  if (rc) return fail(std::string("sfl_run: ") + h->be.error());
+  return check_errors(h);
+}
+
+}  // namespace sfl

@@ -1,0 +1,79 @@
+// TEST-ONLY host build of the same per-env kernel body (sfl_core.h) behind the
+// same C-ABI: libsfl_hostsim.so.  Used by tests/ to check the product
+// algorithm against the CPU oracle in a container without a GPU.  Never loaded
+// by the product package (network-distributed-q-learning_amd/_lib.py only
+// loads libsfl.so and requires a HIP device).
+#include <stdlib.h>
+#include <string.h>
+
+#include <string>
+
+#include "sfl_engine.h"
+
+namespace {
+
+struct HostBackend {
+  std::string err;
+  static int device_count(int* n) {
+    *n = 0;
+    return 0;
+  }
+  const char* error() const { return err.c_str(); }
+  int init(int) { return 0; }
+  void* alloc(size_t bytes) { return calloc(1, bytes); }
+  void free(void* p) { ::free(p); }
+  void h2d(void* d, const void* s, size_t n) { memcpy(d, s, n); }
+  void d2h(void* d, const void* s, size_t n) { memcpy(d, s, n); }
+  void memset(void* p, int v, size_t n) { ::memset(p, v, n); }
+  void fill_f64(double* p, double v, size_t n) {
+    for (size_t i = 0; i < n; ++i) p[i] = v;
+  }
+  void qinit(const sfl::SflMap& m, const sfl::SflState& s, uint32_t n_rows, const uint32_t* port,
+             const uint32_t* state, const double* vals) {
+    for (uint32_t e = 0; e < s.E; ++e)
+      for (uint32_t r = 0; r < n_rows; ++r) {
+        const uint32_t g = port[r], st = state[r];
+        const int w = m.q_w[g];
+        double* row = s.q + (size_t)e * m.q_per_env + m.q_off[g] + (size_t)st * w;
+        for (int j = 0; j < w; ++j) {
+          const double v = vals[(size_t)r * 4 + j];
+          row[j] = (v != v) ? m.default_q : v;
+        }
+        const uint32_t rid = m.row_base[g] + st;
+        s.touched[(size_t)e * m.touched_words + (rid >> 5)] |= 1u << (rid & 31u);
+      }
+  }
+  int run(const sfl::SflMap& m, const sfl::SflState& s, const sfl::SflCtl& c, float* ms) {
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int64_t e = 0; e < (int64_t)s.E; ++e) sfl::env_run(m, s, c, (uint32_t)e);
+    *ms = 0.f;
+    return 0;
+  }
+  int sync() { return 0; }
+};
+
+}  // namespace
+
+using Backend = HostBackend;
+#include "sfl_capi.inc"
+
+// RNG self-test hooks for tests/test_hostsim.py (numpy parity of the device streams)
+extern "C" {
+int sflh_rng_selftest(uint32_t seedseq_value, uint32_t n, uint64_t* out64, uint32_t* out32, double* outd,
+                      uint32_t bound, uint32_t* outb) {
+  sfl::Pcg64 g;
+  sfl::pcg_from_seedseq(seedseq_value, g);
+  for (uint32_t i = 0; i < n; ++i) out64[i] = sfl::pcg_next64(g);
+  sfl::pcg_from_seedseq(seedseq_value, g);
+  for (uint32_t i = 0; i < n; ++i) out32[i] = sfl::pcg_next32(g);
+  sfl::pcg_from_seedseq(seedseq_value, g);
+  for (uint32_t i = 0; i < n; ++i) outd[i] = sfl::pcg_double(g);
+  sfl::pcg_from_seedseq(seedseq_value, g);
+  for (uint32_t i = 0; i < n; ++i) outb[i] = sfl::pcg_bounded(g, bound);
+  return 0;
+}
+int sflh_mf_draw(uint64_t seed, uint64_t tick, uint64_t handle, uint64_t* z) {
+  *z = sfl::mf_draw(seed, tick, handle);
+  return 0;
+}
+}

@@ -665,6 +665,7 @@ class OracleDistrQ:
         self.q: Dict[tuple, list] = {}
         self.trace = trace
         self.events: list = []
+        self.on_step = None  # optional callback(env, obs, action, reward, post) after every env.step
 
     # table primitives (distr_q.py:47-79, 449-490)
     def _row(self, state, agent):
@@ -800,6 +801,8 @@ class OracleDistrQ:
             post = env.step(a)
             if self.trace:
                 self._trace_step(a, post)
+            if self.on_step:
+                self.on_step(env, obs, a, r, post)
             cum += r
         delays = [v[1] for v in env.last_node.values()]
         return cum, len(post["arrived_trains"]), delays
@@ -841,6 +844,8 @@ class OracleDistrQ:
                 post = env.step(action)
                 if self.trace:
                     self._trace_step(action, post)
+                if self.on_step:
+                    self.on_step(env, obs, action, r, post)
                 h = info["active_train"]
                 key = (switch_id(agent), h)
                 if key in pending:
@@ -865,6 +870,57 @@ class OracleDistrQ:
             out["cum_reward_exploit"] = cum_x
             out["arrived_trains_exploit"] = arr_x
         return out
+
+
+def run_decisions(model: "OracleDistrQ", total: int, state: dict = None) -> dict:
+    """The learn loop (distr_q.py:275-362) with episodes restarting as they end, stopped after
+    ``total`` decisions — the product's ``sfl_step`` (the benchmark step).  ``state`` carries the
+    loop across calls; returns it."""
+    env = model.env
+    if state is None:
+        state = dict(rng=np.random.default_rng(model.seed), counts={a: 0 for a in env.agents}, t=0,
+                     in_episode=False, pending={}, at_dest=[], it=None, done=0)
+    rng, counts = state["rng"], state["counts"]
+    while state["done"] < total:
+        if not state["in_episode"]:
+            env.reset(seed=model.seed)
+            if state["t"] == 0:
+                model.init_q_table()
+            state.update(in_episode=True, pending={}, at_dest=[], it=env.agent_iter())
+        try:
+            agent = next(state["it"])
+        except StopIteration:
+            state["in_episode"] = False
+            state["t"] += 1
+            continue
+        obs, rew, term, trunc, info = env.last()
+        r = rew[env.active_train]
+        eps = model.eps0 * (model.eps_decay ** counts[agent])
+        if rng.random() < eps:
+            sub = np.random.Generator(np.random.PCG64(np.random.SeedSequence(int(rng.integers(0, np.iinfo(np.int32).max)))))
+            action = int(sub.choice(np.where(info["action_mask"] == 1)[0]))
+        else:
+            action = model.max_action(obs, agent, info["action_mask"])
+        post = env.step(action)
+        if model.on_step:
+            model.on_step(env, obs, action, r, post)
+        h = info["active_train"]
+        pending, at_dest = state["pending"], state["at_dest"]
+        key = (switch_id(agent), h)
+        if key in pending:
+            p_obs, p_act, p_agent = pending.pop(key)
+            model.update(p_obs, p_act, r, obs, p_agent, agent, counts)
+        pending[(post["next_switch"], h)] = (obs, action, agent)
+        for tr in post["arrived_trains"]:
+            if tr not in at_dest:
+                at_dest.append(tr)
+                for (k_sw, k_tr), (u_obs, u_act, u_agent) in list(pending.items()):
+                    if k_tr == tr:
+                        model.update(u_obs, u_act, model.DESTINATION_BONUS, None, u_agent, None, counts)
+                        del pending[(k_sw, k_tr)]
+        counts[agent] += 1
+        state["done"] += 1
+    return state
 
 
 def sem_digest(semaphores) -> int:
