@@ -332,6 +332,10 @@ struct Env {
       sem_set(p, sem_pack(h, is_in, now, now + span));
   }
   SFL_FN void free_switch_ports(int sw, int h) {
+    if (sw < 0 || sw >= m.S) {
+      err |= E_PORT;
+      return;
+    }
     const int np = m.sw_np[sw];
     for (int j = 0; j < np; ++j) {
       uint64_t r = sem(4 * sw + j);
@@ -666,6 +670,10 @@ SFL_FN void env_tick(Env& v) {
     else if ((st == S_STOPPED || st == S_MALF) && tb_prev(b) == A_STOP) sw = sw_at;
     else if (st == S_STOPPED || st == S_MALF) sw = v.next_port(h) >> 2;
     else continue;
+    if (sw >= m.S) {  // next port is None: the reference would raise here
+      v.err |= E_PORT;
+      continue;
+    }
     v.mask(0, wi) |= bit;
     s.tr_dec[v.ix(h)] = (uint16_t)sw;
   }
@@ -781,8 +789,11 @@ SFL_FN void env_decide(Env& v, Decision& d, bool greedy) {
   const int np = m.sw_np[sw];
   const int na = m.sw_na[sw];
   const int pin = v.next_port(h);
-  if ((pin >> 2) != sw) v.err |= E_PORT;
-  const int slot = pin & 3;
+  int slot = pin & 3;
+  if ((pin >> 2) != sw || slot >= np) {  // observer.py:294-301 (the reference would raise)
+    v.err |= E_PORT;
+    slot = 0;
+  }
   // observe
   uint32_t free_bits = 0;
   for (int j = 0; j < np; ++j) {
