@@ -15,9 +15,14 @@
 
 namespace {
 
-__global__ void __launch_bounds__(256) k_run(sfl::SflMap m, sfl::SflState s, sfl::SflCtl c) {
+// The three parameter structs live in device memory and are passed by pointer: a by-value
+// struct whose fields are reached through references would be copied to scratch per lane.
+// NW = 32-bit words of the per-env train bitmasks kept in registers (T <= 32 * NW).
+template <int NW>
+__global__ void __launch_bounds__(256) k_run(const sfl::SflMap* __restrict__ m, const sfl::SflState* __restrict__ s,
+                                             const sfl::SflCtl* __restrict__ c) {
   const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e < s.E) sfl::env_run(m, s, c, e);
+  if (e < s->E) sfl::env_run<NW>(*m, *s, *c, e);
 }
 
 __global__ void k_fill_f64(double* p, double v, size_t n) {
@@ -44,6 +49,7 @@ __global__ void k_qinit(sfl::SflMap m, sfl::SflState s, uint32_t n_rows, const u
 struct HipBackend {
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  void* d_params = nullptr;  // device copies of SflMap | SflState | SflCtl
   std::string err;
   int dev = 0;
 
@@ -69,11 +75,13 @@ struct HipBackend {
     if (!check(hipSetDevice(device), "hipSetDevice")) return -1;
     if (!check(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking), "hipStreamCreate")) return -1;
     if (!check(hipEventCreate(&ev0), "hipEventCreate") || !check(hipEventCreate(&ev1), "hipEventCreate")) return -1;
+    if (!check(hipMalloc(&d_params, 4096), "hipMalloc params")) return -1;
     return 0;
   }
   ~HipBackend() {
     if (ev0) hipEventDestroy(ev0);
     if (ev1) hipEventDestroy(ev1);
+    if (d_params) hipFree(d_params);
     if (stream) hipStreamDestroy(stream);
   }
   void* alloc(size_t bytes) {
@@ -102,9 +110,30 @@ struct HipBackend {
     check(hipGetLastError(), "k_qinit");
   }
   int run(const sfl::SflMap& m, const sfl::SflState& s, const sfl::SflCtl& c, float* ms) {
+    static_assert(sizeof(sfl::SflMap) + sizeof(sfl::SflState) + sizeof(sfl::SflCtl) + 64 < 4096, "params");
     const unsigned blocks = (s.E + 255) / 256;
+    char* base = (char*)d_params;
+    const size_t om = 0, os = (sizeof(sfl::SflMap) + 63) / 64 * 64,
+                 oc = os + (sizeof(sfl::SflState) + 63) / 64 * 64;
+    struct {
+      sfl::SflMap m;
+      char p0[(sizeof(sfl::SflMap) + 63) / 64 * 64 - sizeof(sfl::SflMap)];
+      sfl::SflState s;
+      char p1[(sizeof(sfl::SflState) + 63) / 64 * 64 - sizeof(sfl::SflState)];
+      sfl::SflCtl c;
+    } host_params;
+    host_params.m = m;
+    host_params.s = s;
+    host_params.c = c;
+    (void)om;
+    check(hipMemcpyAsync(d_params, &host_params, sizeof(host_params), hipMemcpyHostToDevice, stream), "params h2d");
     check(hipEventRecord(ev0, stream), "event");
-    k_run<<<blocks, 256, 0, stream>>>(m, s, c);
+    const auto* pm = (const sfl::SflMap*)(base);
+    const auto* ps = (const sfl::SflState*)(base + os);
+    const auto* pc = (const sfl::SflCtl*)(base + oc);
+    if (m.T <= 32) k_run<1><<<blocks, 256, 0, stream>>>(pm, ps, pc);
+    else if (m.T <= 64) k_run<2><<<blocks, 256, 0, stream>>>(pm, ps, pc);
+    else k_run<4><<<blocks, 256, 0, stream>>>(pm, ps, pc);
     if (!check(hipGetLastError(), "k_run launch")) return -1;
     check(hipEventRecord(ev1, stream), "event");
     if (!check(hipEventSynchronize(ev1), "k_run")) return -1;

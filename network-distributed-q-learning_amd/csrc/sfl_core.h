@@ -216,7 +216,9 @@ SFL_FN bool off_map_state(uint32_t s) { return s == S_WAITING || s == S_READY ||
 // ---------------------------------------------------------------------------
 // environment view
 // ---------------------------------------------------------------------------
+template <int NW>
 struct Env {
+  static constexpr int kNW = NW;  // train bitmask words held in registers (T <= 32*NW)
   const SflMap& m;
   const SflState& s;
   const uint32_t e;
@@ -225,8 +227,46 @@ struct Env {
   int32_t now;      // rail_env._elapsed_steps
   uint32_t flags;
   uint32_t epoch;
+  // train bitmasks kept in registers for the whole launch: 0 decision queue, 1 arrived,
+  // 2 destination bonus paid, 3 in malfunction at the previous tick
+  uint32_t msk[4][NW];
 
-  SFL_FN Env(const SflMap& m_, const SflState& s_, uint32_t e_) : m(m_), s(s_), e(e_), E(s_.E), err(0), now(0), flags(0), epoch(0) {}
+  SFL_FN Env(const SflMap& m_, const SflState& s_, uint32_t e_) : m(m_), s(s_), e(e_), E(s_.E), err(0), now(0), flags(0), epoch(0) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int w = 0; w < NW; ++w) msk[k][w] = 0;
+  }
+  SFL_FN void masks_load() {
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int w = 0; w < NW; ++w) msk[k][w] = s.masks[((size_t)k * MAXW + w) * E + e];
+  }
+  SFL_FN void masks_store() const {
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int w = 0; w < NW; ++w) s.masks[((size_t)k * MAXW + w) * E + e] = msk[k][w];
+  }
+  // constant-index access to the register masks (a runtime index would spill them to scratch)
+  SFL_FN bool mbit(int k, int h) const {
+    bool r = false;
+#pragma unroll
+    for (int w = 0; w < NW; ++w)
+      if (w == (h >> 5)) r = (msk[k][w] >> (h & 31)) & 1u;
+    return r;
+  }
+  SFL_FN void mset(int k, int h) {
+#pragma unroll
+    for (int w = 0; w < NW; ++w)
+      if (w == (h >> 5)) msk[k][w] |= 1u << (h & 31);
+  }
+  SFL_FN void mclr(int k, int h) {
+#pragma unroll
+    for (int w = 0; w < NW; ++w)
+      if (w == (h >> 5)) msk[k][w] &= ~(1u << (h & 31));
+  }
   SFL_FN size_t ix(size_t i) const { return i * (size_t)E + e; }
 
   // grid -----------------------------------------------------------------
@@ -288,7 +328,6 @@ struct Env {
   SFL_FN uint16_t& prev_port(int h) const { return s.tr_prev[ix(h)]; }
   SFL_FN uint16_t& src_port(int h) const { return s.tr_src[ix(h)]; }
   SFL_FN uint32_t state_of(int h) const { return tb_state(s.tr_bits[ix(h)]); }
-  SFL_FN uint32_t& mask(int kind, int w) const { return s.masks[((size_t)kind * MAXW + w) * E + e]; }
 
   // semaphores ---------------------------------------------------------------
   SFL_FN uint64_t& sem(int p) const { return s.sem[ix(p)]; }
@@ -421,10 +460,27 @@ struct Env {
   }
 };
 
+// constant-index bit ops on small register arrays (runtime indices would spill them to scratch)
+template <int N>
+SFL_FN bool bget(const uint32_t (&a)[N], int i) {
+  bool r = false;
+#pragma unroll
+  for (int w = 0; w < N; ++w)
+    if (w == (i >> 5)) r = (a[w] >> (i & 31)) & 1u;
+  return r;
+}
+template <int N>
+SFL_FN void bset(uint32_t (&a)[N], int i) {
+#pragma unroll
+  for (int w = 0; w < N; ++w)
+    if (w == (i >> 5)) a[w] |= 1u << (i & 31);
+}
+
 // ---------------------------------------------------------------------------
 // episode reset (switch_env.py:93-158, _init_ports 507-568)
 // ---------------------------------------------------------------------------
-SFL_FN void env_reset(Env& v) {
+template <class V>
+SFL_FN void env_reset(V& v) {
   const SflMap& m = v.m;
   const SflState& s = v.s;
   v.now = 0;
@@ -444,8 +500,10 @@ SFL_FN void env_reset(Env& v) {
     const int p = m.tr_init_port[h];
     v.sem_set(p, sem_pack(h, 1, m.tr_ed[h] - 2, m.tr_ed[h] + m.tr_init_dist[h]));
   }
+#pragma unroll
   for (int k = 0; k < 4; ++k)
-    for (int w = 0; w < MAXW; ++w) v.mask(k, w) = 0;
+#pragma unroll
+    for (int w = 0; w < V::kNW; ++w) v.msk[k][w] = 0;
   // new (switch, train) epoch: slots from older episodes read as empty
   v.epoch = (v.epoch + 1u) & 0xFFu;
   if (v.epoch == 0) {
@@ -464,12 +522,14 @@ SFL_FN void env_reset(Env& v) {
 // (switch_env.py:296-401, 427-485; flatland_lite.RailEnv.step)
 // ---------------------------------------------------------------------------
 // sc_aux layout: pa 0-3 | ddir 4-5 | mover 6 | allowed 7 | given 8-11 | has_pred 12 | pred_valid 13
-SFL_FN void env_tick(Env& v) {
+template <class V>
+SFL_FN void env_tick(V& v) {
   const SflMap& m = v.m;
   const SflState& s = v.s;
   const int32_t t = ++v.now;
   const uint64_t seed = s.seed[v.e];
-  uint32_t movers[MAXW] = {0, 0, 0, 0};
+  constexpr int NW = V::kNW;
+  uint32_t movers[NW] = {};
 
   // pass 1: plan pop + prediction (switch_env.py:304-339), malfunction draw, action
   // preprocessing, desired move, cell claims (flatland step, first agent loop)
@@ -490,7 +550,7 @@ SFL_FN void env_tick(Env& v) {
         v.plan(h) = pl_pop(p);
       }
       if (pos >= 0) {
-        Env::Move mv = v.check_action(given, pos, (int)dir);
+        typename V::Move mv = v.check_action(given, pos, (int)dir);
         aux |= 1u << 12;
         if (mv.valid) {
           aux |= 1u << 13;
@@ -522,14 +582,14 @@ SFL_FN void env_tick(Env& v) {
       ddir = m.tr_init_dir[h];
       mover = true;
     } else if (saved != 0 && update_allowed) {
-      Env::Move mv = v.check_action(saved, pos, (int)dir);
+      typename V::Move mv = v.check_action(saved, pos, (int)dir);
       desired = mv.cell;
       ddir = (uint32_t)mv.dir;
       pa = saved;
       mover = desired != pos;
     }
     if (mover) {
-      movers[h >> 5] |= 1u << (h & 31);
+      bset(movers, h);
       uint8_t& c = s.claim[v.ix(desired)];
       if (c == 0xFF) c = (uint8_t)h;
     }
@@ -541,11 +601,12 @@ SFL_FN void env_tick(Env& v) {
   }
 
   // pass 2: motion check, least fixed point (flatland_lite.motion_check)
-  uint32_t allowed[MAXW] = {0, 0, 0, 0};
+  uint32_t allowed[NW] = {};
   bool changed = true;
   while (changed) {
     changed = false;
-    for (int w = 0; w < MAXW; ++w) {
+#pragma unroll
+    for (int w = 0; w < V::kNW; ++w) {
       uint32_t pend = movers[w] & ~allowed[w];
       while (pend) {
         const int h = w * 32 + ctz32(pend);
@@ -553,7 +614,7 @@ SFL_FN void env_tick(Env& v) {
         const int32_t d = s.sc_desired[v.ix(h)];
         if (s.claim[v.ix(d)] != (uint8_t)h) continue;
         const uint8_t j = s.occ[v.ix(d)];
-        if (j == 0xFF || (((movers[j >> 5] & allowed[j >> 5]) >> (j & 31)) & 1u)) {
+        if (j == 0xFF || (bget(movers, j) && bget(allowed, j))) {
           allowed[w] |= 1u << (h & 31);
           changed = true;
         }
@@ -575,7 +636,7 @@ SFL_FN void env_tick(Env& v) {
     const bool mover = (aux >> 6) & 1u;
     if (mover && s.claim[v.ix(desired)] == (uint8_t)h) s.claim[v.ix(desired)] = 0xFF;
     const bool in_mf = mf > 0;
-    bool ma = in_mf ? false : (mover && ((allowed[h >> 5] >> (h & 31)) & 1u));
+    bool ma = in_mf ? false : (mover && bget(allowed, h));
     const bool valid_move = is_moving_action(pa) && ma;
     const bool ed_reached = t >= m.tr_ed[h];
     const uint32_t prev_st = st;
@@ -605,10 +666,8 @@ SFL_FN void env_tick(Env& v) {
         if (npos == m.tr_target[h]) st = S_DONE;
       }
     }
-    const int wi = h >> 5;
-    const uint32_t bit = 1u << (h & 31);
-    if (st == S_DONE && !(v.mask(1, wi) & bit)) {
-      v.mask(1, wi) |= bit;  // arrived (position None, arrival_time set)
+    if (st == S_DONE && !v.mbit(1, h)) {
+      v.mset(1, h);  // arrived (position None, arrival_time set)
       npos = -1;
     }
     if (npos != pos) {
@@ -649,19 +708,17 @@ SFL_FN void env_tick(Env& v) {
       const int p = v.next_port(h);
       if (!sem_present(v.sem(p))) v.sem_set(p, sem_pack(h, 1, t, t + m.tr_init_dist[h]));
     }
-    const int wi = h >> 5;
-    const uint32_t bit = 1u << (h & 31);
     if (tb_mf(b) > 0) {
-      if (!(v.mask(3, wi) & bit)) new_mf++;
-      v.mask(3, wi) |= bit;
+      if (!v.mbit(3, h)) new_mf++;
+      v.mset(3, h);
     } else {
-      v.mask(3, wi) &= ~bit;
+      v.mclr(3, h);
     }
     const int32_t pos = v.pos(h);
     if (pos < 0 || st == S_WAITING) continue;
     const uint32_t p = v.plan(h);
     const uint32_t nxt = pl_len(p) ? pl_front(p) : A_FWD;
-    Env::Move mv = v.check_action(nxt, pos, (int)tb_dir(b));
+    typename V::Move mv = v.check_action(nxt, pos, (int)tb_dir(b));
     if (mv.cell < 0) continue;
     const int sw_at = m.cell_sw[mv.cell];
     if (sw_at < 0) continue;
@@ -674,7 +731,7 @@ SFL_FN void env_tick(Env& v) {
       v.err |= E_PORT;
       continue;
     }
-    v.mask(0, wi) |= bit;
+    v.mset(0, h);
     s.tr_dec[v.ix(h)] = (uint16_t)sw;
   }
   s.n_mf[v.e] += new_mf;
@@ -682,10 +739,12 @@ SFL_FN void env_tick(Env& v) {
   if (terminated) v.flags |= F_TERM;
 }
 
-SFL_FN bool queue_empty(const Env& v) {
-  for (int w = 0; w < MAXW; ++w)
-    if (v.mask(0, w)) return false;
-  return true;
+template <class V>
+SFL_FN bool queue_empty(const V& v) {
+  uint32_t any = 0;
+#pragma unroll
+  for (int w = 0; w < V::kNW; ++w) any |= v.msk[0][w];
+  return any == 0;
 }
 
 // ---------------------------------------------------------------------------
@@ -701,7 +760,8 @@ struct Decision {
 };
 
 // value of full-row action a (the full row is default_q except the compact entries)
-SFL_FN double row_val(const Env& v, int sw, int slot, const double* row, int a) {
+template <class V>
+SFL_FN double row_val(const V& v, int sw, int slot, const double* row, int a) {
   const SflMap& m = v.m;
   const int na = m.sw_na[sw];
   if (a == na - 1) return row[m.q_w[4 * sw + slot] - 1];
@@ -710,7 +770,8 @@ SFL_FN double row_val(const Env& v, int sw, int slot, const double* row, int a) 
 }
 
 // np.argmax over the full row, falling back to the first allowed maximum (distr_q.py:468-490)
-SFL_FN int max_action(const Env& v, int sw, int slot, const double* row, const uint32_t amask) {
+template <class V>
+SFL_FN int max_action(const V& v, int sw, int slot, const double* row, const uint32_t amask) {
   const int na = v.m.sw_na[sw];
   int best = 0;
   double mx = row_val(v, sw, slot, row, 0);
@@ -736,7 +797,8 @@ SFL_FN int max_action(const Env& v, int sw, int slot, const double* row, const u
 }
 
 // max(row) over the full, unmasked row (distr_q.py:449-466)
-SFL_FN double row_max(const Env& v, int sw, int slot, const double* row) {
+template <class V>
+SFL_FN double row_max(const V& v, int sw, int slot, const double* row) {
   const int na = v.m.sw_na[sw];
   double mx = row_val(v, sw, slot, row, 0);
   for (int a = 1; a < na; ++a) {
@@ -747,7 +809,8 @@ SFL_FN double row_max(const Env& v, int sw, int slot, const double* row) {
 }
 
 // rail_network.py:246-278 + 303-416
-SFL_FN int transition_train(Env& v, int h, int in_p, int out_p) {
+template <class V>
+SFL_FN int transition_train(V& v, int h, int in_p, int out_p) {
   const SflMap& m = v.m;
   const int target = m.port_nb[out_p];
   if (v.state_of(h) != S_MALF) {
@@ -772,19 +835,21 @@ SFL_FN int transition_train(Env& v, int h, int in_p, int out_p) {
   return target >> 2;
 }
 
-SFL_FN void env_decide(Env& v, Decision& d, bool greedy) {
+template <class V>
+SFL_FN void env_decide(V& v, Decision& d, bool greedy) {
   const SflMap& m = v.m;
   const SflState& s = v.s;
   // agent_iter: lowest queued train (switch_env.py:418-421, 616-622)
-  int h = 0;
-  for (int w = 0; w < MAXW; ++w) {
-    uint32_t mk = v.mask(0, w);
-    if (mk) {
+  int h = -1;
+#pragma unroll
+  for (int w = 0; w < V::kNW; ++w) {
+    const uint32_t mk = v.msk[0][w];
+    if (h < 0 && mk) {
       h = w * 32 + ctz32(mk);
-      v.mask(0, w) = mk & (mk - 1u);
-      break;
+      v.msk[0][w] = mk & (mk - 1u);
     }
   }
+  if (h < 0) h = 0;
   const int sw = s.tr_dec[v.ix(h)];
   const int np = m.sw_np[sw];
   const int na = m.sw_na[sw];
@@ -886,7 +951,7 @@ SFL_FN void env_decide(Env& v, Decision& d, bool greedy) {
     const uint32_t a = pl_at(p, i);
     if (a == A_STOP) continue;
     if (pc < 0) break;
-    Env::Move mv = v.check_action(a, pc, pd);
+    typename V::Move mv = v.check_action(a, pc, pd);
     pc = mv.cell;
     pd = mv.dir;
   }
@@ -908,7 +973,8 @@ SFL_FN void env_decide(Env& v, Decision& d, bool greedy) {
 }
 
 // post-step part of the learn loop (distr_q.py:322-362)
-SFL_FN void env_post(Env& v, const Decision& d) {
+template <class V>
+SFL_FN void env_post(V& v, const Decision& d) {
   const SflMap& m = v.m;
   const SflState& s = v.s;
   uint64_t& here = s.slot[v.ix((size_t)d.sw * m.T + d.h)];
@@ -938,10 +1004,11 @@ SFL_FN void env_post(Env& v, const Decision& d) {
   uint64_t& nxt = s.slot[v.ix((size_t)d.next_sw * m.T + d.h)];
   nxt = slot_make(pend_make((uint32_t)d.sw, (uint32_t)d.slot, d.state, (uint32_t)d.j), slot_rew(nxt, v.epoch), v.epoch);
   // destination bonus for newly arrived trains (distr_q.py:344-356)
-  for (int w = 0; w < MAXW; ++w) {
-    uint32_t fresh = v.mask(1, w) & ~v.mask(2, w);
+#pragma unroll
+  for (int w = 0; w < V::kNW; ++w) {
+    uint32_t fresh = v.msk[1][w] & ~v.msk[2][w];
     if (!fresh) continue;
-    v.mask(2, w) |= fresh;
+    v.msk[2][w] |= fresh;
     while (fresh) {
       const int tr = w * 32 + ctz32(fresh);
       fresh &= fresh - 1u;
@@ -967,7 +1034,8 @@ SFL_FN void env_post(Env& v, const Decision& d) {
 }
 
 // order-independent checksum of the semaphore table (trace/debug only)
-SFL_FN uint64_t sem_checksum(const Env& v) {
+template <class V>
+SFL_FN uint64_t sem_checksum(const V& v) {
   uint64_t c = 0;
   for (int p = 0; p < v.m.NP; ++p) {
     const uint64_t r = v.sem(p);
@@ -976,7 +1044,8 @@ SFL_FN uint64_t sem_checksum(const Env& v) {
   return c;
 }
 
-SFL_FN void trace_decision(const Env& v, const SflCtl& c, const Decision& d) {
+template <class V>
+SFL_FN void trace_decision(const V& v, const SflCtl& c, const Decision& d) {
   const uint64_t n = *c.trace_n;
   if (n < (uint64_t)c.trace_cap) {
     uint64_t* t = c.trace + 4 * n;
@@ -989,11 +1058,22 @@ SFL_FN void trace_decision(const Env& v, const SflCtl& c, const Decision& d) {
   *c.trace_n = n + 1;
 }
 
+// any lane of the wave (host build: a wave of one lane)
+SFL_FN bool wave_any(bool pred) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __ballot(pred) != 0ull;
+#else
+  return pred;
+#endif
+}
+
 // ---------------------------------------------------------------------------
 // driver: one env until its episode target / decision budget
 // ---------------------------------------------------------------------------
+template <int NW>
 SFL_FN void env_run(const SflMap& m, const SflState& s, const SflCtl& c, uint32_t e) {
-  Env v(m, s, e);
+  using V = Env<NW>;
+  V v(m, s, e);
   v.flags = s.eflags[e];
   v.now = s.elapsed[e];
   v.epoch = s.epoch[e];
@@ -1005,7 +1085,9 @@ SFL_FN void env_run(const SflMap& m, const SflState& s, const SflCtl& c, uint32_
   d.state = 0;
   double cum = s.cum_reward[e];
   const bool test_mode = c.mode == 1;
+  v.masks_load();
   while (true) {
+    const bool busy = wave_any(phase == PH_DECIDE || phase == PH_POST);
     if (phase == PH_RESET) {
       // learn: optional greedy round before episode t (distr_q.py:278-281)
       if (test_mode) {
@@ -1021,33 +1103,46 @@ SFL_FN void env_run(const SflMap& m, const SflState& s, const SflCtl& c, uint32_
       cum = 0.0;
       phase = PH_TICK;
     } else if (phase == PH_TICK) {
-      int live = m.T;
-      for (int w = 0; w < MAXW; ++w) live -= popc32(v.mask(1, w));
-      abytes += 36ull * (uint64_t)live;
-      env_tick(v);
-      ticks++;
-      if (v.flags & F_TERM) phase = (v.flags & F_INFLIGHT) ? PH_POST : PH_END;
-      else if (!queue_empty(v)) phase = (v.flags & F_INFLIGHT) ? PH_POST : PH_DECIDE;
-    } else if (phase == PH_DECIDE) {
-      env_decide(v, d, (v.flags & F_GREEDY) != 0);
-      abytes += 220ull + 48ull * m.sw_np[d.sw] + 8ull * m.sw_na[d.sw];
-      v.flags |= F_INFLIGHT;
-      phase = queue_empty(v) ? PH_TICK : PH_POST;
-    } else if (phase == PH_POST) {
-      if (!(v.flags & F_GREEDY)) env_post(v, d);
-      if (c.trace && (int32_t)e == c.trace_env) trace_decision(v, c, d);
-      v.flags &= ~F_INFLIGHT;
-      cum += (double)d.reward;
-      s.ep_dec[e] += 1;
-      s.dec_total[e] += 1;
-      s.step_ctr[e] += 1;
-      if (s.step_ctr[e] > m.max_steps) v.flags |= F_TRUNC;
-      dec++;
-      phase = (v.flags & (F_TERM | F_TRUNC)) ? PH_END : PH_DECIDE;
-      if (c.dec_budget > 0 && (int64_t)dec >= c.dec_budget) break;
+      // Wave-synchronised ticking: a lane that needs a Flatland tick waits while any lane of
+      // its wave still has queued decisions, so the (expensive) tick body runs once per
+      // round for the whole wave instead of in almost every iteration.  Scheduling only:
+      // each env's own sequence of operations is unchanged.
+      if (!busy) {
+        int live = m.T;
+#pragma unroll
+        for (int w = 0; w < V::kNW; ++w) live -= popc32(v.msk[1][w]);
+        abytes += 36ull * (uint64_t)live;
+        env_tick(v);
+        ticks++;
+        if (v.flags & F_TERM) phase = (v.flags & F_INFLIGHT) ? PH_POST : PH_END;
+        else if (!queue_empty(v)) phase = (v.flags & F_INFLIGHT) ? PH_POST : PH_DECIDE;
+      }
+    } else if (phase == PH_DECIDE || phase == PH_POST) {
+      bool post_now = phase == PH_POST;
+      if (phase == PH_DECIDE) {
+        env_decide(v, d, (v.flags & F_GREEDY) != 0);
+        abytes += 220ull + 48ull * m.sw_np[d.sw] + 8ull * m.sw_na[d.sw];
+        v.flags |= F_INFLIGHT;
+        if (queue_empty(v)) phase = PH_TICK;  // ticks happen between the step and the update
+        else post_now = true;
+      }
+      if (post_now) {
+        if (!(v.flags & F_GREEDY)) env_post(v, d);
+        if (c.trace && (int32_t)e == c.trace_env) trace_decision(v, c, d);
+        v.flags &= ~F_INFLIGHT;
+        cum += (double)d.reward;
+        s.ep_dec[e] += 1;
+        s.dec_total[e] += 1;
+        s.step_ctr[e] += 1;
+        if (s.step_ctr[e] > m.max_steps) v.flags |= F_TRUNC;
+        dec++;
+        phase = (v.flags & (F_TERM | F_TRUNC)) ? PH_END : PH_DECIDE;
+        if (c.dec_budget > 0 && (int64_t)dec >= c.dec_budget) break;
+      }
     } else {  // PH_END
       int arrived = 0;
-      for (int w = 0; w < MAXW; ++w) arrived += popc32(v.mask(1, w));
+#pragma unroll
+      for (int w = 0; w < V::kNW; ++w) arrived += popc32(v.msk[1][w]);
       const size_t cap = (size_t)(c.stats_cap > 0 ? c.stats_cap : 1);
       if (v.flags & F_GREEDY) {
         if (test_mode) {
@@ -1088,6 +1183,7 @@ SFL_FN void env_run(const SflMap& m, const SflState& s, const SflCtl& c, uint32_
       phase = PH_RESET;
     }
   }
+  v.masks_store();
   s.phase[e] = phase;
   s.elapsed[e] = v.now;
   s.eflags[e] = v.flags;

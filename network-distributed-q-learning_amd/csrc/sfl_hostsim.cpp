@@ -45,7 +45,11 @@ struct HostBackend {
   }
   int run(const sfl::SflMap& m, const sfl::SflState& s, const sfl::SflCtl& c, float* ms) {
 #pragma omp parallel for schedule(dynamic, 1)
-    for (int64_t e = 0; e < (int64_t)s.E; ++e) sfl::env_run(m, s, c, (uint32_t)e);
+    for (int64_t e = 0; e < (int64_t)s.E; ++e) {
+      if (m.T <= 32) sfl::env_run<1>(m, s, c, (uint32_t)e);
+      else if (m.T <= 64) sfl::env_run<2>(m, s, c, (uint32_t)e);
+      else sfl::env_run<4>(m, s, c, (uint32_t)e);
+    }
     *ms = 0.f;
     return 0;
   }

@@ -15,7 +15,7 @@
 
 #ifndef SFL_FN
 #if defined(__HIPCC__)
-#define SFL_FN __host__ __device__ inline
+#define SFL_FN __host__ __device__ inline __attribute__((always_inline))
 #else
 #define SFL_FN inline
 #endif
