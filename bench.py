@@ -44,6 +44,23 @@ def cpu_baseline(sc, seconds: float):
                        f"(from episode start, incl. the Q-table init)")
 
 
+def pmc_traffic():
+    """HBM bytes per k_run launch from the committed rocprofv3 PMC summary of this exact kernel source
+    (profiles/*_pmc.json written by scripts/pmc_summary.py), or None."""
+    import glob
+    import hashlib
+    core = os.path.join(REPO, PKG, "csrc", "sfl_core.h")
+    sha = hashlib.sha1(open(core, "rb").read()).hexdigest()
+    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc.json")), reverse=True):
+        try:
+            d = json.load(open(f))
+        except Exception:
+            continue
+        if d.get("source_sha1") == sha:
+            return d["traffic_bytes_per_launch"], os.path.relpath(f, REPO)
+    return None, None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -56,17 +73,11 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
-    else:
-        torch.cuda.set_device(0)
+    par = importlib.import_module(PKG + ".parallel")
+    world, rank, local = par.world()
+    dist = par.init("nccl")
+    torch.cuda.set_device(local)
 
     mapgen = importlib.import_module(PKG + ".mapgen")
     comp = importlib.import_module(PKG + ".compiler")
@@ -74,7 +85,7 @@ def main():
     sc = mapgen.make_config(args.config)
     cm = comp.compile_scenario(sc)
     E = args.envs
-    seeds = [450565 + rank * E + i for i in range(E)]
+    seeds = par.shard_seeds(450565, E, rank)
     b = runtime.Batch(cm, HP, seeds, device=local)
     b.learn_begin()
     b.apply_qinit()
@@ -98,19 +109,12 @@ def main():
         abytes += b.counters()["last_launch_alg_bytes"]
     barrier()
     dt = time.perf_counter() - t0
-    if dist is not None:
-        t = torch.tensor([dt, float(total)], dtype=torch.float64, device="cuda")
-        mx = t.clone()
-        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-        sm = t.clone()
-        dist.all_reduce(sm, op=dist.ReduceOp.SUM)
-        dt, total_all = float(mx[0]), float(sm[1])
-    else:
-        total_all = float(total)
+    dt, total_all = par.reduce_timing(dist, dt, float(total), device="cuda")
     if rank == 0:
         avg_ms = kms / max(1, args.steps)
         bytes_per_launch = abytes / max(1, args.steps)
         achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+        traffic, traffic_src = pmc_traffic()
         res = {
             "metric": METRIC,
             "value": total_all / dt,
@@ -130,7 +134,7 @@ def main():
                        "envs_per_gpu": E, "decisions_per_env_per_step": args.decisions,
                        "parallelism": f"env-batch dp{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": "k_run", "avg_kernel_ms": avg_ms,
                          "alg_bytes_per_launch": bytes_per_launch},
         }

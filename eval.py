@@ -1,0 +1,41 @@
+"""Greedy evaluation of saved models (the reference's eval.py).
+
+Usage: python eval.py EXP_DIR [EXP_DIR ...] [--model checkpoint_3000.pkl]
+Each EXP_DIR holds the config.ini of its run; results go to EXP_DIR/eval_<i>/ (10 evaluations
+when malfunctions are on, else 1, as in eval.py:85-97).
+"""
+import argparse
+import configparser
+import importlib
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+PKG = "network-distributed-q-learning_amd"
+ASyncSwitchEnv = importlib.import_module(PKG + ".env").ASyncSwitchEnv
+DistrQLearning = importlib.import_module(PKG + ".distr_q").DistrQLearning
+from main import build_scenario  # noqa: E402
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("exp_dirs", nargs="+")
+    ap.add_argument("--model", default="distr_q_model.pkl")
+    args = ap.parse_args()
+    for exp_dir in args.exp_dirs:
+        print(f"Evaluating {exp_dir}")
+        config = configparser.ConfigParser()
+        config.read(os.path.join(exp_dir, "config.ini"))
+        env = ASyncSwitchEnv(build_scenario(config), render_mode="human", max_steps=100_000)
+        m = config["MODEL"]
+        model = DistrQLearning(env=env, gamma=float(m["gamma"]), epsilon=float(m["epsilon"]),
+                               epsilon_decay_rate=float(m["epsilon_decay_rate"]), lr=float(m["lr"]),
+                               lr_decay_rate=float(m["lr_decay_rate"]), default_q=float(m["default_q"]),
+                               seed=int(config["MISC"]["random_seed"]))
+        model.load(os.path.join(exp_dir, args.model))
+        num_evals = 10 if float(config["ENV"].get("malfunction_rate", 0)) > 0 else 1
+        for i in range(num_evals):
+            print(f"Eval {i + 1}")
+            out_dir = os.path.join(exp_dir, f"eval_{i}")
+            os.makedirs(out_dir, exist_ok=True)
+            model.test(out_dir=out_dir, plot=False)
+            print("")

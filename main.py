@@ -1,0 +1,66 @@
+"""Launch a training run from an ini file (the reference's main.py -c config.ini).
+
+Sections/keys as in the reference (main.py:21-60; writer hyperparam_tuning.py:49-82):
+  [MISC]  random_seed, out_dir, checkpoint_freq, exploit_freq   (+ optional n_envs, device)
+  [ENV]   width, height, max_num_cities, max_rails_between_cities, max_rail_pairs_in_city,
+          number_of_agents, malfunction_rate, min_duration, max_duration   (+ optional scenario:
+          a mapgen config name or a scenario JSON path, used instead of the size keys)
+  [MODEL] gamma, epsilon, epsilon_decay_rate, lr, lr_decay_rate, default_q, num_episodes
+"""
+import argparse
+import configparser
+import importlib
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+PKG = "network-distributed-q-learning_amd"
+mapgen = importlib.import_module(PKG + ".mapgen")
+ASyncSwitchEnv = importlib.import_module(PKG + ".env").ASyncSwitchEnv
+DistrQLearning = importlib.import_module(PKG + ".distr_q").DistrQLearning
+
+
+def build_scenario(config):
+    env = config["ENV"]
+    seed = int(config["MISC"]["random_seed"])
+    mf = (float(env.get("malfunction_rate", 0)), int(env.get("min_duration", 0)), int(env.get("max_duration", 0)))
+    if "scenario" in env:
+        s = env["scenario"]
+        sc = mapgen.make_config(s, seed=seed, malfunction=mf) if s in mapgen.CONFIGS else mapgen.Scenario.load(s)
+        return sc
+    return mapgen.from_flatland_params(int(env["width"]), int(env["height"]), int(env["max_num_cities"]),
+                                       int(env["number_of_agents"]), seed, malfunction=mf)
+
+
+def launch_experiment(config_path):
+    start_time = time.time()
+    config = configparser.ConfigParser()
+    config.read(config_path)
+    out_dir = config["MISC"]["out_dir"]
+    os.makedirs(out_dir, exist_ok=True)
+    checkpoint_freq = int(config["MISC"]["checkpoint_freq"])
+    exploit_freq = int(config["MISC"]["exploit_freq"])
+    n_envs = int(config["MISC"].get("n_envs", 1))
+    device = int(config["MISC"].get("device", 0))
+    env = ASyncSwitchEnv(build_scenario(config), render_mode="human", max_steps=100_000, n_envs=n_envs, device=device)
+    m = config["MODEL"]
+    model = DistrQLearning(env=env, gamma=float(m["gamma"]), epsilon=float(m["epsilon"]),
+                           epsilon_decay_rate=float(m["epsilon_decay_rate"]), lr=float(m["lr"]),
+                           lr_decay_rate=float(m["lr_decay_rate"]), default_q=float(m["default_q"]),
+                           seed=int(config["MISC"]["random_seed"]))
+    n_ep = int(m["num_episodes"])
+    model.learn(num_episodes=n_ep, out_dir=out_dir, checkpoint_freq=checkpoint_freq, exploit_freq=exploit_freq)
+    model.save(os.path.join(out_dir, "distr_q_model.pkl"))
+    elapsed_time = time.time() - start_time
+    print("DONE!")
+    print(f"TOTAL TIME: {elapsed_time:.1f} seconds")
+    print(f"Seconds per episode: {elapsed_time / n_ep:.1f}")
+    print(f"Device (kernel) time: {env.flatland_step_time:.3f} seconds")
+
+
+if __name__ == "__main__":
+    parser = argparse.ArgumentParser()
+    parser.add_argument("-c", "--config", type=str, help="Config file path", required=True)
+    args = parser.parse_args()
+    launch_experiment(args.config)

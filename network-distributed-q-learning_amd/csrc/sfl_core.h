@@ -127,7 +127,8 @@ struct SflCtl {
   int32_t mode;          // 0 = learn, 1 = greedy test
   int32_t exploit_freq;  // learn: greedy round before episode t when (t+1) % f == 0
   int32_t ep_target;     // stop once this many episodes of the mode are done (-1: unlimited)
-  int32_t stats_cap;     // rows in the stats buffers (episode index modulo cap)
+  int32_t stats_cap;     // rows in the stats buffers: row = (episode index - stats_base) % cap
+  int32_t stats_base;
   int64_t dec_budget;    // decisions per env in this launch (<= 0: unlimited)
   double* st_cum;        // [cap][E]
   int32_t* st_arrived;   // [cap][E]
@@ -1148,7 +1149,7 @@ SFL_FN void env_run(const SflMap& m, const SflState& s, const SflCtl& c, uint32_
         if (test_mode) {
           const int32_t i = s.n_test[e];
           if (c.st_cum && c.stats_cap > 0) {
-            const size_t row = (size_t)i % cap;
+            const size_t row = (size_t)(i - c.stats_base) % cap;
             c.st_cum[row * s.E + e] = cum;
             c.st_arrived[row * s.E + e] = arrived;
             c.st_mf[row * s.E + e] = s.n_mf[e];
@@ -1160,7 +1161,7 @@ SFL_FN void env_run(const SflMap& m, const SflState& s, const SflCtl& c, uint32_
         } else {
           const int32_t i = s.ep_t[e];
           if (c.sx_cum && c.stats_cap > 0) {
-            const size_t row = (size_t)i % cap;
+            const size_t row = (size_t)(i - c.stats_base) % cap;
             c.sx_cum[row * s.E + e] = cum;
             c.sx_arrived[row * s.E + e] = arrived;
           }
@@ -1169,7 +1170,7 @@ SFL_FN void env_run(const SflMap& m, const SflState& s, const SflCtl& c, uint32_
       } else {
         const int32_t i = s.ep_t[e];
         if (c.st_cum && c.stats_cap > 0) {
-          const size_t row = (size_t)i % cap;
+          const size_t row = (size_t)(i - c.stats_base) % cap;
           c.st_cum[row * s.E + e] = cum;
           c.st_arrived[row * s.E + e] = arrived;
           c.st_mf[row * s.E + e] = s.n_mf[e];

@@ -308,6 +308,7 @@ int run(Handle<B>* h, const SflCtl& c_in, sfl_run_args* args) {
     return p;
   };
   c.stats_cap = cap;
+  c.stats_base = c_in.stats_base;
   if (args && cap > 0) {
     c.st_cum = (double*)scr((size_t)cap * E * 8);
     c.st_arrived = (int32_t*)scr((size_t)cap * E * 4);

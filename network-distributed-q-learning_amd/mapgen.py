@@ -441,3 +441,18 @@ MAP_SEED = 450565  # the reference default seed (test_model.py:30)
 def make_config(name: str, seed: int = MAP_SEED, malfunction=(0.01, 5, 15)) -> Scenario:
     kw = dict(CONFIGS[name])
     return generate(seed=seed, malfunction=malfunction, name=name, **kw)
+
+
+def from_flatland_params(width: int, height: int, max_num_cities: int, number_of_agents: int, seed: int,
+                         malfunction=(0.0, 0, 0), spacing: int = 5, margin: int = 3) -> Scenario:
+    """Scenario for the reference's [ENV] config keys (main.py:21-60).
+
+    Flatland's sparse_rail_generator is absent, so the city layout is replaced by a line
+    grid of the same size: as many lines as fit in ``width`` x ``height``, one station per
+    city, ``number_of_agents`` trains."""
+    size = max(int(width), int(height))
+    n_lines = max(3, (size - 2 * margin - 1) // spacing + 1)
+    n_sw = n_lines * n_lines - 4
+    return generate(n_switches=n_sw, n_trains=int(number_of_agents), n_stations=max(1, int(max_num_cities)),
+                    seed=int(seed), nx_lines=n_lines, ny_lines=n_lines, spacing=spacing, margin=margin,
+                    size=size, malfunction=malfunction, name=f"flatland_{width}x{height}")

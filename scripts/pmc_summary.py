@@ -1,0 +1,42 @@
+"""Summarise rocprofv3 PMC passes for k_run into a JSON (HBM traffic per launch, gfx950-corrected).
+
+FETCH_SIZE / WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE counts 64 B per 128-B request, i.e. half the
+bytes of a wide coalesced stream (MI355X_MICROARCH.md §HBM) — we apply that x2 correction and note
+that other access widths are uncalibrated.
+Usage: python scripts/pmc_summary.py gpurun_out/<tag> profiles/<name>.json
+"""
+import csv
+import glob
+import hashlib
+import json
+import os
+import statistics
+import sys
+
+
+def main(src, dst):
+    vals = {}
+    for d in sorted(glob.glob(os.path.join(src, "pmc_*"))):
+        for f in glob.glob(os.path.join(d, "*counter_collection.csv")):
+            for r in csv.DictReader(open(f)):
+                if "k_run" in r["Kernel_Name"]:
+                    vals.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
+    med = {k: statistics.median(v[1:] if len(v) > 1 else v) for k, v in vals.items()}  # skip the warm-up launch
+    core = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                        "network-distributed-q-learning_amd", "csrc", "sfl_core.h")
+    out = {"kernel": "k_run", "per_launch_median": med,
+           "fetch_bytes_corrected": 2 * med.get("FETCH_SIZE", 0) * 1024,
+           "write_bytes": med.get("WRITE_SIZE", 0) * 1024,
+           "source_sha1": hashlib.sha1(open(core, "rb").read()).hexdigest(),
+           "note": "FETCH_SIZE x2 (gfx950 half-count of 128-B requests); uncalibrated for narrow scattered access"}
+    out["traffic_bytes_per_launch"] = out["fetch_bytes_corrected"] + out["write_bytes"]
+    if "TCC_HIT_sum" in med:
+        out["l2_hit_rate"] = med["TCC_HIT_sum"] / max(1.0, med["TCC_HIT_sum"] + med["TCC_MISS_sum"])
+    if "SQ_WAVE_CYCLES" in med:
+        out["wait_fraction"] = med.get("SQ_WAIT_ANY", 0) / med["SQ_WAVE_CYCLES"]
+    json.dump(out, open(dst, "w"), indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2])

@@ -1,0 +1,44 @@
+"""Train on the small default map (the reference's test_model.py, same hyper-parameters).
+
+Usage: python test_model.py [out_dir] [--envs E] [--episodes N]
+The reference builds an 18x18, 5-city, 2-train Flatland map (test_model.py:29-46); Flatland
+is not available, so the synthetic 18x18 'c1' scenario stands in for it.
+"""
+import argparse
+import importlib
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+PKG = "network-distributed-q-learning_amd"
+mapgen = importlib.import_module(PKG + ".mapgen")
+ASyncSwitchEnv = importlib.import_module(PKG + ".env").ASyncSwitchEnv
+DistrQLearning = importlib.import_module(PKG + ".distr_q").DistrQLearning
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("out_dir", nargs="?", default=os.path.join("out", "test_model"))
+    ap.add_argument("--envs", type=int, default=1)
+    ap.add_argument("--episodes", type=int, default=5)
+    args = ap.parse_args()
+    out_dir = args.out_dir
+    os.makedirs(out_dir, exist_ok=True)
+
+    random_seed = 450565
+    rail_env = mapgen.make_config("c1", seed=random_seed, malfunction=(0.01, 5, 15))
+    num_episodes = args.episodes
+
+    # -------------------------------------------------------------------------------------
+    env = ASyncSwitchEnv(rail_env, render_mode="human", max_steps=100_000, n_envs=args.envs)
+    model = DistrQLearning(env=env, gamma=1., epsilon=0.5, epsilon_decay_rate=0.9997, lr=0.1,
+                           lr_decay_rate=1.0, default_q=0., seed=random_seed)
+    start_time = time.time()
+    model.learn(num_episodes=num_episodes, out_dir=out_dir, checkpoint_freq=10000)
+    model.save(os.path.join(out_dir, "distr_q_model.pkl"))
+    elapsed_time = time.time() - start_time
+    print("DONE!")
+    print(f"TOTAL TIME: {elapsed_time:.1f} seconds")
+    print(f"Seconds per episode: {elapsed_time / num_episodes:.1f}")
+    print(f"Device (kernel) time: {env.flatland_step_time:.3f} seconds")
+    print(f"Total step time: {env.step_time:.1f} seconds")
