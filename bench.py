@@ -45,12 +45,10 @@ def cpu_baseline(sc, seconds: float):
 
 
 def pmc_traffic():
-    """HBM bytes per k_run launch from the committed rocprofv3 PMC summary of this exact kernel source
+    """HBM bytes per env-kernel launch from the committed rocprofv3 PMC summary of this exact kernel source
     (profiles/*_pmc.json written by scripts/pmc_summary.py), or None."""
     import glob
-    import hashlib
-    core = os.path.join(REPO, PKG, "csrc", "sfl_core.h")
-    sha = hashlib.sha1(open(core, "rb").read()).hexdigest()
+    sha = importlib.import_module(PKG + ".build").kernel_source_sha1()
     for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc.json")), reverse=True):
         try:
             d = json.load(open(f))
@@ -102,6 +100,9 @@ def main():
     total = 0
     kms = 0.0
     abytes = 0
+    cnt0 = b.counters()
+    kname = (f"k_wave<{cnt0['kernel_variant']}> (one env per wavefront)" if cnt0["kernel_variant"] > 0
+             else "k_run (one env per lane)")
     for _ in range(args.steps):
         n, ms = b.step(args.decisions)
         total += n
@@ -135,7 +136,7 @@ def main():
                        "parallelism": f"env-batch dp{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
-                         "kernel": "k_run", "avg_kernel_ms": avg_ms,
+                         "kernel": kname, "avg_kernel_ms": avg_ms,
                          "alg_bytes_per_launch": bytes_per_launch},
         }
         if world == 1 and not args.no_cpu:

@@ -114,6 +114,8 @@ typedef struct {
   uint64_t last_launch_ticks;
   uint64_t last_launch_alg_bytes; /* sum of 220+48P+8A per decision + 36*T_live per env-tick */
   double last_kernel_ms;      /* device time of the last run/step launch (HIP events) */
+  int32_t kernel_variant;     /* 0: one env per lane (k_run); v > 0: one env per lane group (k_wave shape v) */
+  int32_t group_lanes;        /* lanes per env */
 } sfl_counters;
 
 int sfl_abi_version(void);

@@ -54,7 +54,7 @@ class RunArgs(C.Structure):
 class Counters(C.Structure):
     _fields_ = [("decisions", C.c_uint64), ("last_launch_decisions", C.c_uint64),
                 ("last_launch_ticks", C.c_uint64), ("last_launch_alg_bytes", C.c_uint64),
-                ("last_kernel_ms", C.c_double)]
+                ("last_kernel_ms", C.c_double), ("kernel_variant", C.c_int32), ("group_lanes", C.c_int32)]
 
 
 EXPORTS = {

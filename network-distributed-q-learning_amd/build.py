@@ -9,8 +9,17 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("SFL_ARCH", "gfx950")
-SOURCES = ["sfl.hip", "sfl_core.h", "sfl_rng.h", "sfl_engine.h", "sfl_capi.inc", "sfl_hostsim.cpp",
+SOURCES = ["sfl.hip", "sfl_core.h", "sfl_wave.h", "sfl_rng.h", "sfl_engine.h", "sfl_capi.inc", "sfl_hostsim.cpp",
            os.path.join("..", "..", "include", "sfl.h")]
+
+
+def kernel_source_sha1() -> str:
+    """Hash of the device-code sources: ties a committed profile (profiles/*_pmc.json) to the kernel it measured."""
+    import hashlib
+    h = hashlib.sha1()
+    for f in ("sfl.hip", "sfl_core.h", "sfl_wave.h", "sfl_rng.h"):
+        h.update(open(os.path.join(CSRC, f), "rb").read())
+    return h.hexdigest()
 
 
 def _stale(out: str, srcs) -> bool:

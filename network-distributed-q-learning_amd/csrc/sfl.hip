@@ -12,6 +12,11 @@
 #include <string>
 
 #include "sfl_engine.h"
+#include "sfl_wave.h"
+
+#ifndef SFL_WAVE_OCC
+#define SFL_WAVE_OCC 4  // waves per SIMD the one-env-per-wave kernel is register-budgeted for
+#endif
 
 namespace {
 
@@ -23,6 +28,14 @@ __global__ void __launch_bounds__(256) k_run(const sfl::SflMap* __restrict__ m, 
                                              const sfl::SflCtl* __restrict__ c) {
   const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e < s->E) sfl::env_run<NW>(*m, *s, *c, e);
+}
+
+// One env per wavefront (sfl_wave.h): 4 envs per block.  PPL / SPL = semaphore / counter
+// registers per lane (sfl::kVariants).
+template <int PPL, int SPL>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SFL_WAVE_OCC))) k_wave(const sfl::SflMap* __restrict__ m, const sfl::SflState* __restrict__ s,
+                                              const sfl::SflCtl* __restrict__ c) {
+  sfl::wave::run<PPL, SPL>(*m, *s, *c);
 }
 
 __global__ void k_fill_f64(double* p, double v, size_t n) {
@@ -47,6 +60,7 @@ __global__ void k_qinit(sfl::SflMap m, sfl::SflState s, uint32_t n_rows, const u
 }
 
 struct HipBackend {
+  static constexpr bool kHasWave = true;
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   void* d_params = nullptr;  // device copies of SflMap | SflState | SflCtl
@@ -109,7 +123,7 @@ struct HipBackend {
     k_qinit<<<blocks, 256, 0, stream>>>(m, s, n_rows, port, state, vals);
     check(hipGetLastError(), "k_qinit");
   }
-  int run(const sfl::SflMap& m, const sfl::SflState& s, const sfl::SflCtl& c, float* ms) {
+  int run(const sfl::SflMap& m, const sfl::SflState& s, const sfl::SflCtl& c, int variant, float* ms) {
     static_assert(sizeof(sfl::SflMap) + sizeof(sfl::SflState) + sizeof(sfl::SflCtl) + 64 < 4096, "params");
     const unsigned blocks = (s.E + 255) / 256;
     char* base = (char*)d_params;
@@ -131,7 +145,11 @@ struct HipBackend {
     const auto* pm = (const sfl::SflMap*)(base);
     const auto* ps = (const sfl::SflState*)(base + os);
     const auto* pc = (const sfl::SflCtl*)(base + oc);
-    if (m.T <= 32) k_run<1><<<blocks, 256, 0, stream>>>(pm, ps, pc);
+    const unsigned wblocks = (unsigned)(((size_t)s.E * 64 + 255) / 256);
+    if (variant == 1) k_wave<sfl::kVariants[1].PPL, sfl::kVariants[1].SPL><<<wblocks, 256, 0, stream>>>(pm, ps, pc);
+    else if (variant == 2) k_wave<sfl::kVariants[2].PPL, sfl::kVariants[2].SPL><<<wblocks, 256, 0, stream>>>(pm, ps, pc);
+    else if (variant == 3) k_wave<sfl::kVariants[3].PPL, sfl::kVariants[3].SPL><<<wblocks, 256, 0, stream>>>(pm, ps, pc);
+    else if (m.T <= 32) k_run<1><<<blocks, 256, 0, stream>>>(pm, ps, pc);
     else if (m.T <= 64) k_run<2><<<blocks, 256, 0, stream>>>(pm, ps, pc);
     else k_run<4><<<blocks, 256, 0, stream>>>(pm, ps, pc);
     if (!check(hipGetLastError(), "k_run launch")) return -1;

@@ -6,6 +6,7 @@
 #pragma once
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <string>
@@ -38,6 +39,7 @@ struct Handle {
   uint64_t* d_launch_ticks = nullptr;
   uint64_t* d_launch_bytes = nullptr;
   float last_kernel_ms = 0.f;
+  int variant = 0;  // 0: k_run (lane per env); v > 0: k_wave shape kVariants[v] (see choose_variant)
 
   template <class T>
   T* dalloc(size_t n) {
@@ -58,6 +60,38 @@ struct Handle {
   }
 };
 
+// One-env-per-wavefront kernel shapes (sfl_wave.h): PPL semaphore and SPL counter registers
+// per lane (ports <= 64*PPL, switches <= 64*SPL).  Index 0 = the lane-per-env kernel (k_run).
+struct WaveShape {
+  int PPL, SPL;
+};
+constexpr WaveShape kVariants[] = {{0, 0}, {1, 1}, {4, 1}, {8, 2}};
+constexpr int kNumVariants = 4;
+
+// Eligibility: trains fit one lane each (T <= 64, 64-bit masks), the env fits the variant's
+// registers and every semaphore time fits the 11-bit register field.  SFL_KERNEL=scalar
+// forces k_run.
+inline int choose_variant(const sfl_map_desc* md, bool backend_has_wave) {
+  if (!backend_has_wave) return 0;
+  const char* env = getenv("SFL_KERNEL");
+  if (env && strcmp(env, "scalar") == 0) return 0;
+  if (md->T > 64) return 0;
+  int32_t ed_max = 0, ed_min = 0, dist_max = 0, len_max = 0;
+  for (int32_t h = 0; h < md->T; ++h) {
+    ed_max = md->tr_ed[h] > ed_max ? md->tr_ed[h] : ed_max;
+    ed_min = md->tr_ed[h] < ed_min ? md->tr_ed[h] : ed_min;
+    dist_max = md->tr_init_dist[h] > dist_max ? md->tr_init_dist[h] : dist_max;
+  }
+  for (int32_t p = 0; p < md->S * 4; ++p) len_max = md->port_len[p] > len_max ? md->port_len[p] : len_max;
+  const int64_t span = (int64_t)(dist_max > 2 * len_max + 2 ? dist_max : 2 * len_max + 2) + 4;
+  const int64_t t_hi = (int64_t)(ed_max > md->max_episode_steps ? ed_max : md->max_episode_steps) + 2 + span;
+  if (t_hi > 1023 || ed_min - 2 < -1024) return 0;
+  for (int v = 1; v < kNumVariants; ++v) {
+    if (md->S * 4 <= 64 * kVariants[v].PPL && md->S <= 64 * kVariants[v].SPL) return v;
+  }
+  return 0;
+}
+
 template <class B>
 int create(const sfl_map_desc* md, const sfl_hparams* hp, uint32_t n_envs, const uint64_t* env_seeds, int device,
            Handle<B>** out) {
@@ -72,6 +106,7 @@ int create(const sfl_map_desc* md, const sfl_hparams* hp, uint32_t n_envs, const
     return fail(std::string("sfl_create: backend init failed: ") + h->be.error());
   }
   h->E = n_envs;
+  h->variant = choose_variant(md, B::kHasWave);
   SflMap& m = h->map;
   const size_t HW = (size_t)md->H * md->W, NP = (size_t)md->S * 4, S = md->S, T = md->T;
   m.H = md->H;
@@ -345,7 +380,7 @@ int run(Handle<B>* h, const SflCtl& c_in, sfl_run_args* args) {
     c.trace_cap = args->trace_cap;
   }
   float ms = 0.f;
-  int rc = h->be.run(h->map, h->st, c, &ms);
+  int rc = h->be.run(h->map, h->st, c, h->variant, &ms);
   h->last_kernel_ms = ms;
   if (!rc && args && cap > 0) {
     if (args->cum_reward) h->be.d2h(args->cum_reward, c.st_cum, (size_t)cap * E * 8);

@@ -13,6 +13,7 @@
 namespace {
 
 struct HostBackend {
+  static constexpr bool kHasWave = false;  // the host build runs the lane-per-env body only
   std::string err;
   static int device_count(int* n) {
     *n = 0;
@@ -43,7 +44,7 @@ struct HostBackend {
         s.touched[(size_t)e * m.touched_words + (rid >> 5)] |= 1u << (rid & 31u);
       }
   }
-  int run(const sfl::SflMap& m, const sfl::SflState& s, const sfl::SflCtl& c, float* ms) {
+  int run(const sfl::SflMap& m, const sfl::SflState& s, const sfl::SflCtl& c, int /*variant*/, float* ms) {
 #pragma omp parallel for schedule(dynamic, 1)
     for (int64_t e = 0; e < (int64_t)s.E; ++e) {
       if (m.T <= 32) sfl::env_run<1>(m, s, c, (uint32_t)e);

@@ -182,7 +182,7 @@ class Batch:
         self.lib.check(self.lib.dll.sfl_get_counters(self.h, C.byref(c)), "sfl_get_counters")
         return dict(decisions=c.decisions, last_launch_decisions=c.last_launch_decisions,
                     last_launch_ticks=c.last_launch_ticks, last_launch_alg_bytes=c.last_launch_alg_bytes,
-                    last_kernel_ms=c.last_kernel_ms)
+                    last_kernel_ms=c.last_kernel_ms, kernel_variant=c.kernel_variant, group_lanes=c.group_lanes)
 
     # ---- Q-table export / import (the reference's pickle dict, distr_q.py:521-527) -------------
     def q_raw(self, env: int) -> Tuple[np.ndarray, np.ndarray]:

@@ -1,4 +1,4 @@
-"""Summarise rocprofv3 PMC passes for k_run into a JSON (HBM traffic per launch, gfx950-corrected).
+"""Summarise rocprofv3 PMC passes for the env kernel (k_run / k_wave) into a JSON (HBM traffic per launch, gfx950-corrected).
 
 FETCH_SIZE / WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE counts 64 B per 128-B request, i.e. half the
 bytes of a wide coalesced stream (MI355X_MICROARCH.md §HBM) — we apply that x2 correction and note
@@ -7,7 +7,7 @@ Usage: python scripts/pmc_summary.py gpurun_out/<tag> profiles/<name>.json
 """
 import csv
 import glob
-import hashlib
+import importlib
 import json
 import os
 import statistics
@@ -16,18 +16,20 @@ import sys
 
 def main(src, dst):
     vals = {}
+    kname = None
     for d in sorted(glob.glob(os.path.join(src, "pmc_*"))):
         for f in glob.glob(os.path.join(d, "*counter_collection.csv")):
             for r in csv.DictReader(open(f)):
-                if "k_run" in r["Kernel_Name"]:
+                if "k_run" in r["Kernel_Name"] or "k_wave" in r["Kernel_Name"]:
+                    kname = r["Kernel_Name"]
                     vals.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
     med = {k: statistics.median(v[1:] if len(v) > 1 else v) for k, v in vals.items()}  # skip the warm-up launch
-    core = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
-                        "network-distributed-q-learning_amd", "csrc", "sfl_core.h")
-    out = {"kernel": "k_run", "per_launch_median": med,
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    build = importlib.import_module("network-distributed-q-learning_amd.build")
+    out = {"kernel": kname, "per_launch_median": med,
            "fetch_bytes_corrected": 2 * med.get("FETCH_SIZE", 0) * 1024,
            "write_bytes": med.get("WRITE_SIZE", 0) * 1024,
-           "source_sha1": hashlib.sha1(open(core, "rb").read()).hexdigest(),
+           "source_sha1": build.kernel_source_sha1(),
            "note": "FETCH_SIZE x2 (gfx950 half-count of 128-B requests); uncalibrated for narrow scattered access"}
     out["traffic_bytes_per_launch"] = out["fetch_bytes_corrected"] + out["write_bytes"]
     if "TCC_HIT_sum" in med:

@@ -25,12 +25,28 @@ def lib():
     return _lib.load_product()
 
 
+@pytest.fixture(params=["wave", "scalar"])
+def kernel(request, monkeypatch):
+    """Which device kernel a Batch created inside the test runs (chosen at sfl_create):
+    'wave' = one env per wavefront (k_wave, the default where eligible), 'scalar' = k_run."""
+    if request.param == "scalar":
+        monkeypatch.setenv("SFL_KERNEL", "scalar")
+    else:
+        monkeypatch.delenv("SFL_KERNEL", raising=False)
+    return request.param
+
+
+def _check_kernel(b, kernel):
+    c = b.counters()
+    assert (c["kernel_variant"] > 0) == (kernel == "wave"), c
+
+
 def _q(items):
     return {tuple(k): v for k, v in items}
 
 
 @pytest.mark.parametrize("name", CASES)
-def test_golden_env0_and_trace(lib, name):
+def test_golden_env0_and_trace(lib, kernel, name):
     g = _golden.load(name)
     hp = g["hparams"]
     cm = comp.compile_scenario(g["scenario_obj"])
@@ -38,6 +54,7 @@ def test_golden_env0_and_trace(lib, name):
     b = runtime.Batch(cm, hp, [g["seed"], seed1, seed1 + 1], lib=lib, max_steps=hp.get("max_steps", 100_000),
                       ntab=4096)
     b.trace_env = 1
+    _check_kernel(b, kernel)
     out = b.learn(g["n_episodes"], exploit_freq=g["exploit_freq"])
     ref = g["learn"]["outputs"]
     assert out["cum_reward"][:, 0].tolist() == ref["cum_reward"]
@@ -58,7 +75,7 @@ def test_golden_env0_and_trace(lib, name):
     assert b.q_dict(0) == _q(g["test"]["q_final"])
 
 
-def test_c2_batch_gpu_equals_host_build_and_oracle(lib):
+def test_c2_batch_gpu_equals_host_build_and_oracle(lib, kernel):
     """512 envs stepped in chunks: every env's Q-table bit-equal to the host build, sampled envs to the oracle."""
     from tests import hostsim
     sc = mapgen.make_config("c2")
@@ -66,6 +83,7 @@ def test_c2_batch_gpu_equals_host_build_and_oracle(lib):
     seeds = [1000 + i for i in range(512)]
     chunks = [37, 91, 250]
     bg = runtime.Batch(cm, HP, seeds, lib=lib, ntab=1 << 14)
+    _check_kernel(bg, kernel)
     bh = runtime.Batch(cm, HP, seeds, lib=hostsim.lib(), ntab=1 << 14)
     for b in (bg, bh):
         b.learn_begin()
@@ -91,6 +109,7 @@ def test_c3_full_size_batch(lib):
     E = 65536
     seeds = [450565 + i for i in range(E)]
     b = runtime.Batch(cm, HP, seeds, lib=lib)
+    assert b.counters()["kernel_variant"] > 0  # the bench kernel
     b.learn_begin()
     b.apply_qinit()
     total = 0
@@ -113,6 +132,7 @@ def test_c5_small_batch(lib):
     cm = comp.compile_scenario(sc)
     seeds = [5, 6, 7, 8]
     b = runtime.Batch(cm, HP, seeds, lib=lib, ntab=1 << 14)
+    assert b.counters()["kernel_variant"] == 0  # 128 trains: lane-per-env kernel
     b.learn_begin()
     b.apply_qinit()
     b.step(150)
