@@ -100,6 +100,7 @@ def main():
     total = 0
     kms = 0.0
     abytes = 0
+    dec_l = ticks_l = 0
     cnt0 = b.counters()
     kname = (f"k_wave<{cnt0['kernel_variant']}> (one env per wavefront)" if cnt0["kernel_variant"] > 0
              else "k_run (one env per lane)")
@@ -107,7 +108,10 @@ def main():
         n, ms = b.step(args.decisions)
         total += n
         kms += ms
-        abytes += b.counters()["last_launch_alg_bytes"]
+        cl = b.counters()
+        abytes += cl["last_launch_alg_bytes"]
+        dec_l += cl["last_launch_decisions"]
+        ticks_l += cl["last_launch_ticks"]
     barrier()
     dt = time.perf_counter() - t0
     dt, total_all = par.reduce_timing(dist, dt, float(total), device="cuda")
@@ -137,7 +141,8 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": kname, "avg_kernel_ms": avg_ms,
-                         "alg_bytes_per_launch": bytes_per_launch},
+                         "alg_bytes_per_launch": bytes_per_launch,
+                         "ticks_per_decision": ticks_l / max(1, dec_l)},
         }
         if world == 1 and not args.no_cpu:
             res["cpu_baseline"] = cpu_baseline(sc, args.cpu_seconds)

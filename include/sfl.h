@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define SFL_ABI_VERSION 1
+#define SFL_ABI_VERSION 2
 
 typedef struct sfl_handle sfl_handle;
 

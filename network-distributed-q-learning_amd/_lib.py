@@ -91,7 +91,7 @@ class Lib:
             fn = getattr(self.dll, name)
             fn.restype = res
             fn.argtypes = args
-        if self.dll.sfl_abi_version() != 1:
+        if self.dll.sfl_abi_version() != 2:
             raise SflError("ABI version mismatch")
 
     def check(self, rc: int, what: str):
@@ -111,7 +111,8 @@ def load_product() -> Lib:
     """The HIP library; raises if it is missing or no GPU is visible (no fallback)."""
     global _product
     if _product is None:
-        lib = Lib(PRODUCT_LIB)
+        # SFL_LIB: an alternative in-tree build of the same HIP sources (tuning sweeps)
+        lib = Lib(os.environ.get("SFL_LIB", PRODUCT_LIB))
         if lib.device_count() < 1:
             raise SflError("libsfl.so loaded but no HIP device is visible: the SwitchFL hot path runs on MI355X only")
         _product = lib

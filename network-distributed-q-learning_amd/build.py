@@ -29,11 +29,13 @@ def _stale(out: str, srcs) -> bool:
     return any(os.path.getmtime(os.path.join(CSRC, s)) > t for s in srcs)
 
 
-def build_hip(force: bool = False, verbose: bool = False) -> str:
-    out = os.path.join(HERE, "libsfl.so")
+def build_hip(force: bool = False, verbose: bool = False, out: str = None, defines=(), flags=()) -> str:
+    """hipcc build of libsfl.so (gfx950).  ``out``/``defines``/``flags``: alternative builds for tuning."""
+    out = out or os.path.join(HERE, "libsfl.so")
     if force or _stale(out, SOURCES):
         cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off",
-               "-Wno-unused-result", "-Wno-unused-value", "-o", out + ".tmp", os.path.join(CSRC, "sfl.hip")]
+               "-Wno-unused-result", "-Wno-unused-value"] + [f"-D{d}" for d in defines] + list(flags) + [
+               "-o", out + ".tmp", os.path.join(CSRC, "sfl.hip")]
         if verbose:
             print(" ".join(cmd), flush=True)
         subprocess.run(cmd, check=True, cwd=CSRC)

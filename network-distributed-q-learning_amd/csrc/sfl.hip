@@ -9,6 +9,8 @@
 // multiply/add, not a contracted FMA).
 #include <hip/hip_runtime.h>
 
+#include <stdio.h>
+
 #include <string>
 
 #include "sfl_engine.h"
@@ -158,6 +160,19 @@ struct HipBackend {
     float t = 0.f;
     hipEventElapsedTime(&t, ev0, ev1);
     *ms = t;
+#ifdef SFL_PROFILE
+    if (variant > 0) {
+      unsigned long long pr[8] = {};
+      hipMemcpyFromSymbol(pr, HIP_SYMBOL(sfl::wave::g_prof), sizeof pr);
+      fprintf(stderr,
+              "[sfl profile] cycles reset %.3e tick %.3e decide %.3e (observe %.3e egreedy %.3e apply %.3e) post %.3e "
+              "total %.3e\n",
+              (double)pr[0], (double)pr[1], (double)pr[2], (double)pr[5], (double)pr[6], (double)pr[7], (double)pr[3],
+              (double)pr[4]);
+      unsigned long long z[8] = {};
+      hipMemcpyToSymbol(HIP_SYMBOL(sfl::wave::g_prof), z, sizeof z);
+    }
+#endif
     return err.empty() ? 0 : -1;
   }
   int sync() { return check(hipStreamSynchronize(stream), "sync") && err.empty() ? 0 : -1; }

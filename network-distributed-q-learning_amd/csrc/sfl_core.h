@@ -81,6 +81,11 @@ struct SflMap {
   const int16_t* tr_init_port;
   const double* eps_tab;
   const double* lr_tab;
+  // packed copies for the one-env-per-wave kernel (sfl_wave.h), built at create time
+  const uint32_t* sw_pack;    // [S][8]: np | na<<4; src/dst 2b per action; turn/j 2b; q_w 4b per slot; row map per slot
+  const uint32_t* port_pack;  // [NP][4]: nb | len<<16; unique | q_w<<16; row_base; q_off
+  const uint32_t* move_tab;   // [H*W][4 dir][4 action&3]: check_action result (see move_pack)
+  const int32_t* tr_pack;     // [T][8]: ed, la, k, target, init_cell, init_dist, init_delay, init_dir | init_port<<16
 };
 
 struct SflState {
@@ -117,7 +122,7 @@ struct SflState {
   uint8_t* occ;         // [H*W][E] occupying train or 0xFF
   uint8_t* claim;       // [H*W][E] motion-check claim or 0xFF
   uint64_t* sem;        // [NP][E] semaphore records
-  uint64_t* slot;       // [S*T][E] pending update | reward | epoch
+  uint64_t* slot;       // pending update | reward | epoch: [S*T][E] (k_run), [E][T][S] (k_wave)
   uint32_t* counts;     // [S][E] agent_num_interactions
   double* q;            // [E][q_per_env]
   uint32_t* touched;    // [E][touched_words] Q-table key set
@@ -211,6 +216,34 @@ SFL_FN uint32_t pend_make(uint32_t s, uint32_t slot, uint32_t state, uint32_t j)
 }
 
 SFL_FN bool is_moving_action(uint32_t a) { return a == A_LEFT || a == A_FWD || a == A_RIGHT; }
+
+// flatland-lite check_action_on_agent for (action, cell, dir), packed for move_tab:
+// new cell + 1 (20 bits; 0 = off the grid) | new dir << 20 | transition valid << 22 | new cell valid << 23.
+// Actions NOTHING (0) and STOP (4) behave alike, so a table row is indexed by action & 3.
+SFL_FN uint32_t move_pack(const uint16_t* grid, int H, int W, uint32_t a, int cell, int dir) {
+  const uint32_t nib = ((uint32_t)grid[cell] >> ((3 - dir) * 4)) & 15u;
+  const int n = popc32(nib);
+  int nd = dir, valid = -1;
+  if (a == A_LEFT) {
+    nd = dir + 3;
+    if (n <= 1) valid = 0;
+  } else if (a == A_RIGHT) {
+    nd = dir + 1;
+    if (n <= 1) valid = 0;
+  }
+  nd &= 3;
+  if (a == A_FWD && n == 1) {
+    nd = 3 - (31 - __builtin_clz(nib));
+    valid = 1;
+  }
+  int r = cell / W, c = cell - r * W;
+  r += (nd == 2) - (nd == 0);
+  c += (nd == 1) - (nd == 3);
+  const int nc = (r < 0 || r >= H || c < 0 || c >= W) ? -1 : r * W + c;
+  const bool ok = nc >= 0 && grid[nc] != 0;
+  const bool v = valid < 0 ? (((nib >> (3 - nd)) & 1u) != 0) : (valid != 0);
+  return (uint32_t)(nc + 1) | ((uint32_t)nd << 20) | ((v ? 1u : 0u) << 22) | ((ok ? 1u : 0u) << 23);
+}
 SFL_FN bool on_map_state(uint32_t s) { return s == S_MOVING || s == S_STOPPED || s == S_MALF; }
 SFL_FN bool off_map_state(uint32_t s) { return s == S_WAITING || s == S_READY || s == S_MF_OFF; }
 

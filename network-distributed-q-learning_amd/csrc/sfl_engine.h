@@ -39,6 +39,7 @@ struct Handle {
   uint64_t* d_launch_ticks = nullptr;
   uint64_t* d_launch_bytes = nullptr;
   float last_kernel_ms = 0.f;
+  std::vector<std::vector<uint32_t>> keep;  // host sources of async uploads, alive until the create() sync
   int variant = 0;  // 0: k_run (lane per env); v > 0: k_wave shape kVariants[v] (see choose_variant)
 
   template <class T>
@@ -86,6 +87,7 @@ inline int choose_variant(const sfl_map_desc* md, bool backend_has_wave) {
   const int64_t span = (int64_t)(dist_max > 2 * len_max + 2 ? dist_max : 2 * len_max + 2) + 4;
   const int64_t t_hi = (int64_t)(ed_max > md->max_episode_steps ? ed_max : md->max_episode_steps) + 2 + span;
   if (t_hi > 1023 || ed_min - 2 < -1024) return 0;
+  if (md->q_per_env >= (1ull << 32) || (int64_t)md->H * md->W >= (1 << 20) - 1) return 0;
   for (int v = 1; v < kNumVariants; ++v) {
     if (md->S * 4 <= 64 * kVariants[v].PPL && md->S <= 64 * kVariants[v].SPL) return v;
   }
@@ -160,6 +162,79 @@ int create(const sfl_map_desc* md, const sfl_hparams* hp, uint32_t n_envs, const
   m.tr_init_port = h->upload(md->tr_init_port, T);
   m.eps_tab = h->upload(hp->eps_tab, (size_t)hp->ntab);
   m.lr_tab = h->upload(hp->lr_tab, (size_t)hp->ntab);
+  {
+    // packed tables for the one-env-per-wave kernel: one scalar load per switch / port / train,
+    // and check_action as a table lookup
+    std::vector<uint32_t> swp(S * 8, 0), pp(NP * 4, 0), mv(HW * 16, 0);
+    std::vector<int32_t> trp(T * 8, 0);
+    bool pack_ok = true;
+    for (size_t sw = 0; sw < S; ++sw) {
+      uint32_t* w = &swp[sw * 8];
+      const int na = md->sw_na[sw];
+      w[0] = (uint32_t)md->sw_np[sw] | ((uint32_t)na << 4);
+      for (int a = 0; a < 8 && a < na - 1; ++a) {  // routes (STOP = action na-1 has no entry)
+        w[1] |= ((uint32_t)md->act_src[sw * 8 + a] & 3u) << (2 * a);
+        w[1] |= ((uint32_t)md->act_dst[sw * 8 + a] & 3u) << (16 + 2 * a);
+        w[2] |= ((uint32_t)md->act_turn[sw * 8 + a] & 3u) << (2 * a);
+        w[2] |= ((uint32_t)md->act_j[sw * 8 + a] & 3u) << (16 + 2 * a);
+      }
+      for (int sl = 0; sl < 4; ++sl) {
+        const uint32_t qw = md->q_w[sw * 4 + sl];
+        w[3] |= (qw & 15u) << (4 * sl);
+        // compact row descriptor: full-row action of each compact column (routes leaving
+        // through this slot in action order, then STOP), and the first default-valued action
+        uint32_t rd = 0, c = 0, mind = 15;
+        for (int a = 0; a < na - 1; ++a) {
+          if (md->act_src[sw * 8 + a] == sl) {
+            if (md->act_j[sw * 8 + a] != c) rd |= 1u << 31;  // columns must follow action order
+            rd |= ((uint32_t)a & 15u) << (4 * c++);
+          } else if (mind == 15) {
+            mind = (uint32_t)a;
+          }
+        }
+        if (qw > 0) {
+          if (c != qw - 1u) rd |= 1u << 31;
+          rd |= ((uint32_t)(na - 1) & 15u) << (4 * c);
+        }
+        rd |= mind << 16;
+        if (rd >> 31) pack_ok = false;
+        w[4 + sl] = rd;
+      }
+    }
+    for (size_t p = 0; p < NP; ++p) {
+      pp[p * 4 + 0] = (uint32_t)(uint16_t)md->port_nb[p] | ((uint32_t)(uint16_t)md->port_len[p] << 16);
+      pp[p * 4 + 1] = (uint32_t)(uint16_t)md->port_unique[p] | ((uint32_t)md->q_w[p] << 16);
+      pp[p * 4 + 2] = md->row_base[p];
+      pp[p * 4 + 3] = (uint32_t)md->q_off[p];
+    }
+    for (size_t c = 0; c < HW; ++c)
+      for (int d = 0; d < 4; ++d)
+        for (int a = 0; a < 4; ++a)
+          mv[(c * 4 + d) * 4 + a] = move_pack(md->grid, md->H, md->W, (uint32_t)a, (int)c, d);
+    for (size_t t = 0; t < T; ++t) {
+      int32_t* w = &trp[t * 8];
+      w[0] = md->tr_ed[t];
+      w[1] = md->tr_la[t];
+      w[2] = md->tr_k[t];
+      w[3] = md->tr_target[t];
+      w[4] = md->tr_init_cell[t];
+      w[5] = md->tr_init_dist[t];
+      w[6] = md->tr_init_delay[t];
+      w[7] = (int32_t)((uint32_t)md->tr_init_dir[t] | ((uint32_t)(uint16_t)md->tr_init_port[t] << 16));
+    }
+    if (!pack_ok) {
+      delete h;
+      return fail("sfl_create: compact Q columns do not follow action order (map compiler mismatch)");
+    }
+    h->keep.push_back(std::move(swp));
+    m.sw_pack = h->upload(h->keep.back().data(), h->keep.back().size());
+    h->keep.push_back(std::move(pp));
+    m.port_pack = h->upload(h->keep.back().data(), h->keep.back().size());
+    h->keep.push_back(std::move(mv));
+    m.move_tab = h->upload(h->keep.back().data(), h->keep.back().size());
+    h->keep.emplace_back(trp.begin(), trp.end());
+    m.tr_pack = (const int32_t*)h->upload(h->keep.back().data(), h->keep.back().size());
+  }
 
   SflState& s = h->st;
   const size_t E = n_envs;

@@ -3,15 +3,17 @@
 // Same operations, in the same per-env order, as env_run in sfl_core.h (the lane-per-env
 // body, kept for T > 64 and for the host test build), but the env's hot state lives in
 // VGPRs for the whole launch:
-//   * lane h holds train h (cell, packed bits, plan, ports, delay);
+//   * lane h holds train h (cell, packed bits, plan, ports, delay, its timetable constants);
 //   * lane p % 64, register p / 64 holds the semaphore record of port p (32-bit packed);
 //   * lane s % 64, register s / 64 holds agent_num_interactions of switch s.
 // A Flatland tick runs train-parallel (one lane per train); conflict resolution, the
 // purge of arrived trains, extend_semaphores and the decision queue are wave ballots and
 // per-lane scans of the lanes' own records.  A decision is wave-uniform: cross-lane reads
-// are v_readlane, the read-only map tables are scalar loads through the constant cache,
-// and only the Q-table, the (switch, train) slots and the distance maps reach L2/HBM.
-// Nothing is replicated across envs in a wave, so there is no divergence between envs.
+// are v_readlane, the read-only map tables are packed per switch / port / train
+// (SflMap::sw_pack, port_pack, tr_pack) and read with one scalar load each, check_action is
+// a table lookup (move_tab), and only the Q-table, the (switch, train) slots and the distance
+// maps reach L2/HBM.  Loads whose results are needed later (the Q row, the pending update's
+// Q cell, the slot word) are issued early and made wave-uniform only where they are used.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -20,11 +22,24 @@
 namespace sfl {
 namespace wave {
 
+#ifdef SFL_PROFILE
+// tuning builds only: wall cycles per phase summed over waves (reset, tick, decide, post, total,
+// decide = observe + egreedy + apply)
+__device__ unsigned long long g_prof[8];
+#define SFL_PT(var) const uint64_t var = (uint64_t)__builtin_amdgcn_s_memtime()
+#define SFL_PACC(k, t0) prof[k] += (uint64_t)__builtin_amdgcn_s_memtime() - (t0)
+#else
+#define SFL_PT(var)
+#define SFL_PACC(k, t0)
+#endif
+
 #define SFL_AS_G __attribute__((address_space(1)))
 #define SFL_AS_C __attribute__((address_space(4)))
 
 template <class T, int N>
 using vec_t = T __attribute__((ext_vector_type(N)));
+using u4 = vec_t<uint32_t, 4>;
+using u8 = vec_t<uint32_t, 8>;
 
 // global memory written by this kernel (explicit global address space: no flat accesses)
 template <class T>
@@ -40,14 +55,9 @@ template <class T>
 __device__ __forceinline__ T ldc(const T* p, size_t i) {
   return ((const SFL_AS_C T*)p)[i];
 }
-__device__ __forceinline__ uint32_t ldc_u8(const uint8_t* p, uint32_t i) {
-  return (ldc((const uint32_t*)p, i >> 2) >> (8u * (i & 3u))) & 0xFFu;
-}
-__device__ __forceinline__ uint32_t ldc_u16(const uint16_t* p, uint32_t i) {
-  return (ldc((const uint32_t*)p, i >> 1) >> (16u * (i & 1u))) & 0xFFFFu;
-}
-__device__ __forceinline__ int32_t ldc_i16(const int16_t* p, uint32_t i) {
-  return (int32_t)(int16_t)ldc_u16((const uint16_t*)p, i);
+template <class V>
+__device__ __forceinline__ V ldcv(const void* p, size_t i) {
+  return ((const SFL_AS_C V*)p)[i];
 }
 
 // wave-uniform values
@@ -82,9 +92,37 @@ __device__ __forceinline__ uint64_t r_to64(uint32_t r) {
   return r_present(r) ? sem_pack(r_owner(r), r_in(r), r_t0(r), r_t1(r)) : 0ull;
 }
 
+// decay**n beyond the host-computed tables (rare): out of line, so the f64 pow expansion does
+// not set the register budget of the whole kernel
+__device__ __attribute__((noinline)) double pow_ool(double base, double n) { return pow(base, n); }
+
 __device__ __forceinline__ int ctz64(uint64_t x) { return __builtin_ctzll(x); }
 __device__ __forceinline__ int popc64(uint64_t x) { return __builtin_popcountll(x); }
 
+// packed switch record (SflMap::sw_pack), wave-uniform
+struct SwRec {
+  u8 w;
+  __device__ __forceinline__ int np() const { return (int)(w[0] & 15u); }
+  __device__ __forceinline__ int na() const { return (int)((w[0] >> 4) & 15u); }
+  __device__ __forceinline__ int src(int a) const { return (int)((w[1] >> (2 * a)) & 3u); }
+  __device__ __forceinline__ int dst(int a) const { return (int)((w[1] >> (16 + 2 * a)) & 3u); }
+  __device__ __forceinline__ uint32_t turn(int a) const { return (w[2] >> (2 * a)) & 3u; }
+  __device__ __forceinline__ int j(int a) const { return (int)((w[2] >> (16 + 2 * a)) & 3u); }
+  __device__ __forceinline__ int q_w(int slot) const { return (int)((w[3] >> (4 * slot)) & 15u); }
+  // compact row of an in-port slot: full-row action of column c in bits 4c..4c+3 (c < q_w),
+  // first full-row action valued default_q in bits 16..19 (15: none)
+  __device__ __forceinline__ uint32_t row_desc(int slot) const { return w[4 + slot]; }
+};
+// packed port record (SflMap::port_pack)
+struct PortRec {
+  u4 w;
+  __device__ __forceinline__ int nb() const { return (int)(int16_t)(w[0] & 0xFFFFu); }
+  __device__ __forceinline__ int len() const { return (int)(int16_t)(w[0] >> 16); }
+  __device__ __forceinline__ int unique() const { return (int)(int16_t)(w[1] & 0xFFFFu); }
+  __device__ __forceinline__ int q_w() const { return (int)(w[1] >> 16); }
+  __device__ __forceinline__ uint32_t row_base() const { return w[2]; }
+  __device__ __forceinline__ uint32_t q_off() const { return w[3]; }
+};
 // PPL semaphore registers (ports <= 64*PPL) and SPL counter registers (switches <= 64*SPL) per lane
 template <int PPL, int SPL>
 struct WEnv {
@@ -99,9 +137,17 @@ struct WEnv {
   uint32_t nprv;  // next port | prev port << 16
   uint32_t sdec;  // source port | decision switch << 16
   int32_t delay;
+  // timetable constants of train `lane` (tr_pack)
+  int32_t t_ed, t_target, t_init_cell;
+  uint32_t t_init;  // init dir | init port << 16
   vec_t<uint32_t, PPL> sem;
   vec_t<uint32_t, SPL> cnt;
   uint32_t lerr;  // error bits seen by this lane (OR-reduced on store)
+  // this env's blocks: Q-table, key-set bitmap, (switch, train) slots (env-major [T][S] here,
+  // so one env's slots are contiguous and a flush over switches is one coalesced access)
+  double* qb;
+  uint32_t* touchb;
+  uint64_t* slotb;
   // wave-uniform env scalars
   int32_t now;
   uint32_t flags, epoch;
@@ -109,21 +155,33 @@ struct WEnv {
   Pcg64 rng;
   double cum;
   int32_t n_mf, ep_dec, ep_ticks;
-  int64_t step_ctr, dec_total;
+  int32_t step_ctr;
+  uint32_t n_dec;  // decisions in this launch (dec_total += n_dec on store)
+#ifdef SFL_PROFILE
+  uint64_t prof[3] = {0, 0, 0};  // decide: observe, epsilon-greedy, apply
+#endif
 
   __device__ WEnv(const SflMap& m_, const SflState& s_, uint32_t e_, int lane_)
-      : m(m_), s(s_), e(e_), E(s_.E), lane(lane_), mine(lane_ < m_.T) {}
+      : m(m_), s(s_), e(e_), E(s_.E), lane(lane_), mine(lane_ < m_.T) {
+    qb = s.q + (size_t)e * m.q_per_env;
+    touchb = s.touched + (size_t)e * m.touched_words;
+    slotb = s.slot + (size_t)e * (uint32_t)(m.S * m.T);
+  }
+  __device__ __forceinline__ uint32_t slot_ix(int sw, int h) const { return (uint32_t)(h * m.S + sw); }
 
   __device__ __forceinline__ size_t ix(size_t i) const { return i * (size_t)E + e; }
 
   // ---- cross-lane access (index wave-uniform) -------------------------------------
-  __device__ __forceinline__ uint32_t sget(int p) const { return rl(sem[p >> 6], p & 63); }
+  __device__ __forceinline__ uint32_t sget(int p) const {
+    uint32_t r = rl(sem[0], p & 63);
+#pragma unroll
+    for (int i = 1; i < PPL; ++i) r = (i == (p >> 6)) ? rl(sem[i], p & 63) : r;
+    return r;
+  }
   __device__ __forceinline__ void sset(int p, uint32_t r) {
-    const int k = p >> 6;
     const bool me = lane == (p & 63);
 #pragma unroll
-    for (int i = 0; i < PPL; ++i)
-      if (i == k) sem[i] = me ? r : sem[i];
+    for (int i = 0; i < PPL; ++i) sem[i] = (me && i == (p >> 6)) ? r : sem[i];
   }
   __device__ __forceinline__ uint32_t cget(int sw) const { return rl(cnt[sw >> 6], sw & 63); }
   __device__ __forceinline__ void cset(int sw, uint32_t v) {
@@ -149,46 +207,27 @@ struct WEnv {
   }
   __device__ __forceinline__ uint32_t state_of(int h) const { return tb_state(rl(bits, h)); }
 
-  // ---- grid (U: wave-uniform arguments -> scalar loads) ---------------------------------
-  template <bool U>
-  __device__ __forceinline__ uint32_t grid_at(int cell) const {
-    return U ? ldc_u16(m.grid, (uint32_t)cell) : (uint32_t)ld(m.grid, (size_t)cell);
-  }
-  __device__ __forceinline__ int move_cell(int cell, int d) const {
-    int r = cell / m.W, cc = cell - r * m.W;
-    r += (d == 2) - (d == 0);
-    cc += (d == 1) - (d == 3);
-    if (r < 0 || r >= m.H || cc < 0 || cc >= m.W) return -1;
-    return r * m.W + cc;
-  }
+  // ---- map records --------------------------------------------------------------------
+  __device__ __forceinline__ SwRec sw_rec(int sw) const { return SwRec{ldcv<u8>(m.sw_pack, (size_t)sw)}; }
+  __device__ __forceinline__ PortRec port_rec(int p) const { return PortRec{ldcv<u4>(m.port_pack, (size_t)p)}; }
+  __device__ __forceinline__ int port_nb(int p) const { return (int)(int16_t)(ldc(m.port_pack, (size_t)p * 4) & 0xFFFFu); }
   struct Move {
     int cell, dir;
     bool valid, cell_ok;
   };
-  // flatland-lite check_action_on_agent
+  __device__ __forceinline__ static Move unpack_move(uint32_t w) {
+    Move mv;
+    mv.cell = (int)(w & 0xFFFFFu) - 1;
+    mv.dir = (int)((w >> 20) & 3u);
+    mv.valid = (w >> 22) & 1u;
+    mv.cell_ok = (w >> 23) & 1u;
+    return mv;
+  }
+  // flatland-lite check_action_on_agent as a table lookup; U: wave-uniform arguments (scalar load)
   template <bool U>
   __device__ __forceinline__ Move check_action(uint32_t a, int cell, int dir) const {
-    const uint32_t nib = (grid_at<U>(cell) >> ((3 - dir) * 4)) & 15u;
-    const int n = __builtin_popcount(nib);
-    int nd = dir, valid = -1;
-    if (a == A_LEFT) {
-      nd = dir + 3;
-      if (n <= 1) valid = 0;
-    } else if (a == A_RIGHT) {
-      nd = dir + 1;
-      if (n <= 1) valid = 0;
-    }
-    nd &= 3;
-    if (a == A_FWD && n == 1) {
-      nd = 3 - (31 - __builtin_clz(nib));
-      valid = 1;
-    }
-    Move mv;
-    mv.cell = move_cell(cell, nd);
-    mv.dir = nd;
-    mv.cell_ok = mv.cell >= 0 && grid_at<U>(mv.cell) != 0;
-    mv.valid = valid < 0 ? (((nib >> (3 - nd)) & 1u) != 0) : (valid != 0);
-    return mv;
+    const size_t i = ((size_t)cell * 4 + (size_t)dir) * 4 + (a & 3u);
+    return unpack_move(U ? ldc(m.move_tab, i) : ld(m.move_tab, i));
   }
   template <bool U>
   __device__ __forceinline__ bool action_ok(uint32_t a, int cell, int dir) const {
@@ -196,12 +235,11 @@ struct WEnv {
     return mv.cell_ok && mv.valid;
   }
   // distance map lookup (wave-uniform)
-  __device__ __forceinline__ int32_t dist(int h, int cell, int dir) {
+  __device__ __forceinline__ int32_t dist(int k, int cell, int dir) {
     if (cell < 0) {
       lerr |= E_INF_DIST;
       return 0;
     }
-    const int32_t k = ldc(m.tr_k, (size_t)h);
     const int32_t d = ldc(m.dist, (((size_t)k * m.H * m.W) + (size_t)cell) * 4 + dir);
     if (d >= DIST_INF) lerr |= E_INF_DIST;
     return d;
@@ -222,6 +260,35 @@ struct WEnv {
     }
     return false;
   }
+  // check_port_blocked for every record at once: lane-parallel over each lane's records, one
+  // ballot per register.  bn: the record blocks a train entering through it (next port),
+  // bo: it blocks a train leaving through it (out port).
+  struct Blocked {
+    uint64_t bn[PPL], bo[PPL];
+    __device__ __forceinline__ bool port(int next_p, int out_p) const {
+      uint64_t n = 0, o = 0;
+#pragma unroll
+      for (int k = 0; k < PPL; ++k) {
+        n = (k == (next_p >> 6)) ? bn[k] : n;
+        o = (k == (out_p >> 6)) ? bo[k] : o;
+      }
+      return (((n >> (next_p & 63)) | (o >> (out_p & 63))) & 1ull) != 0;
+    }
+  };
+  __device__ __forceinline__ Blocked blocked_masks(int h) const {
+    const uint64_t malf = __ballot(mine && tb_state(bits) == S_MALF);
+    Blocked bl;
+#pragma unroll
+    for (int k = 0; k < PPL; ++k) {
+      const uint32_t r = sem[k];
+      const uint32_t ow = r_owner(r);
+      const bool live = r_present(r) && ow != (uint32_t)h && r_t0(r) <= now && now <= r_t1(r);
+      const bool mf = (malf >> ow) & 1ull;
+      bl.bn[k] = __ballot(live && (!r_in(r) || mf));
+      bl.bo[k] = __ballot(live && (r_in(r) || mf));
+    }
+    return bl;
+  }
   // set if absent, else (io == ovr_io or t0 in the future) -> retime in place (io kept)
   __device__ __forceinline__ void put_keep(int p, int h, uint32_t in, int32_t span, uint32_t ovr_in) {
     const uint32_t r = sget(p);
@@ -236,25 +303,13 @@ struct WEnv {
   }
 
   // ---- Q-table ------------------------------------------------------------------------------
-  __device__ __forceinline__ double* qrow(int sw, int slot, uint32_t state) const {
-    const int g = 4 * sw + slot;
-    return s.q + (size_t)e * m.q_per_env + ldc(m.q_off, (size_t)g) + (size_t)state * ldc_u8(m.q_w, (uint32_t)g);
-  }
-  __device__ __forceinline__ void touch(int sw, int slot, uint32_t state) const {
-    const uint32_t row = ldc(m.row_base, (size_t)(4 * sw + slot)) + state;
-    atomicOr(&s.touched[(size_t)e * m.touched_words + (row >> 5)], 1u << (row & 31u));
-  }
-  __device__ __forceinline__ double row_val(int sw, int slot, const vec_t<double, 4>& row, int a) const {
-    const int na = (int)ldc_u8(m.sw_na, (uint32_t)sw);
-    if (a == na - 1) return row[(int)ldc_u8(m.q_w, (uint32_t)(4 * sw + slot)) - 1];
-    if ((int)ldc_u8(m.act_src, (uint32_t)(sw * 8 + a)) == slot) return row[(int)ldc_u8(m.act_j, (uint32_t)(sw * 8 + a))];
-    return m.default_q;
-  }
+  __device__ __forceinline__ double* qbase() const { return qb; }
+  __device__ __forceinline__ void touch_row(uint32_t row) const { atomicOr(&touchb[row >> 5], 1u << (row & 31u)); }
   __device__ __forceinline__ double lr_of(uint32_t n) const {
-    return n < (uint32_t)m.ntab ? ldc(m.lr_tab, (size_t)n) : m.lr0 * pow(m.lr_decay, (double)n);
+    return n < (uint32_t)m.ntab ? ldc(m.lr_tab, (size_t)n) : m.lr0 * pow_ool(m.lr_decay, (double)n);
   }
   __device__ __forceinline__ double lr_of_var(uint32_t n) const {
-    return n < (uint32_t)m.ntab ? ld(m.lr_tab, (size_t)n) : m.lr0 * pow(m.lr_decay, (double)n);
+    return n < (uint32_t)m.ntab ? ld(m.lr_tab, (size_t)n) : m.lr0 * pow_ool(m.lr_decay, (double)n);
   }
 
   // ---- launch-boundary state transfer ---------------------------------------------------------
@@ -266,6 +321,10 @@ struct WEnv {
       nprv = (uint32_t)ld(s.tr_next, ix(lane)) | ((uint32_t)ld(s.tr_prev, ix(lane)) << 16);
       sdec = (uint32_t)ld(s.tr_src, ix(lane)) | ((uint32_t)ld(s.tr_dec, ix(lane)) << 16);
       delay = ld(s.tr_delay, ix(lane));
+      t_ed = ld(m.tr_pack, (size_t)lane * 8 + 0);
+      t_target = ld(m.tr_pack, (size_t)lane * 8 + 3);
+      t_init_cell = ld(m.tr_pack, (size_t)lane * 8 + 4);
+      t_init = (uint32_t)ld(m.tr_pack, (size_t)lane * 8 + 7);
     } else {
       pos = -1;
       bits = 0;
@@ -273,6 +332,8 @@ struct WEnv {
       nprv = 0xFFFFFFFFu;
       sdec = 0xFFFFFFFFu;
       delay = 0;
+      t_ed = t_target = t_init_cell = 0;
+      t_init = 0;
     }
 #pragma unroll
     for (int k = 0; k < PPL; ++k) {
@@ -307,8 +368,8 @@ struct WEnv {
     n_mf = uni(ld(s.n_mf, e));
     ep_dec = uni(ld(s.ep_dec, e));
     ep_ticks = uni(ld(s.ep_ticks, e));
-    step_ctr = uni(ld(s.step_ctr, e));
-    dec_total = uni(ld(s.dec_total, e));
+    step_ctr = (int32_t)uni(ld(s.step_ctr, e));
+    n_dec = 0;
   }
   __device__ __forceinline__ void store(int32_t phase) {
     if (mine) {
@@ -356,8 +417,8 @@ struct WEnv {
       st(s.n_mf, e, n_mf);
       st(s.ep_dec, e, ep_dec);
       st(s.ep_ticks, e, ep_ticks);
-      st(s.step_ctr, e, step_ctr);
-      st(s.dec_total, e, dec_total);
+      st(s.step_ctr, e, (int64_t)step_ctr);
+      st(s.dec_total, e, ld(s.dec_total, e) + (int64_t)n_dec);
     }
   }
 
@@ -366,22 +427,22 @@ struct WEnv {
     now = 0;
     if (mine) {
       pos = -1;
-      bits = tb_make(ld(m.tr_init_dir, lane), S_WAITING, A_NONE, 0, 0, 0);
+      bits = tb_make(t_init & 0xFFu, S_WAITING, A_NONE, 0, 0, 0);
       plan = 0;
-      nprv = (nprv & 0xFFFF0000u) | (uint32_t)(uint16_t)ld(m.tr_init_port, lane);
-      delay = ld(m.tr_init_delay, lane);
+      nprv = (nprv & 0xFFFF0000u) | (t_init >> 16);
+      delay = ld(m.tr_pack, (size_t)lane * 8 + 6);
     }
     sem = 0u;
     for (int h = 0; h < m.T; ++h) {
-      const int32_t ed = ldc(m.tr_ed, (size_t)h);
-      sset(ldc_i16(m.tr_init_port, (uint32_t)h), r_pack(h, 1, ed - 2, ed + ldc(m.tr_init_dist, (size_t)h)));
+      const vec_t<int32_t, 8> tr = ldcv<vec_t<int32_t, 8>>(m.tr_pack, (size_t)h);
+      sset((int)((uint32_t)tr[7] >> 16), r_pack(h, 1, tr[0] - 2, tr[0] + tr[5]));
     }
     flags &= ~(F_TERM | F_TRUNC | F_OWN_SCAN | F_INFLIGHT);
     q_mask = arr_mask = fl_mask = mf_mask = 0;
     // new (switch, train) epoch: slots from older episodes read as empty
     epoch = (epoch + 1u) & 0xFFu;
     if (epoch == 0) {
-      for (int i = lane; i < m.S * m.T; i += 64) st(s.slot, ix(i), slot_make(PEND_NONE, 0, 0));
+      for (int i = lane; i < m.S * m.T; i += 64) st(slotb, (size_t)i, slot_make(PEND_NONE, 0, 0));
       epoch = 1;
     }
     cum = 0.0;
@@ -397,17 +458,12 @@ struct WEnv {
     const int32_t t = ++now;
     const uint64_t seed = s.seed[e];
     const int h = lane;
+    const uint32_t t_init_dir = t_init & 0xFFu;
     // pass 1: plan pop + prediction, malfunction draw, action preprocessing, desired move
     bool mover = false;
     int32_t desired = -1, pred = -1;
     uint32_t aux = 0;
-    int32_t t_init_cell = 0, t_target = -1, t_ed = 0;
-    uint32_t t_init_dir = 0;
     if (mine) {
-      t_init_cell = ld(m.tr_init_cell, h);
-      t_init_dir = ld(m.tr_init_dir, h);
-      t_target = ld(m.tr_target, h);
-      t_ed = ld(m.tr_ed, h);
       const uint32_t b = bits;
       const int32_t p0 = pos;
       uint32_t st_ = tb_state(b), dir = tb_dir(b), prev = tb_prev(b), saved = tb_saved(b), mf = tb_mf(b);
@@ -562,8 +618,8 @@ struct WEnv {
     while (D) {
       const int j = ctz64(D);
       D &= D - 1ull;
-      const int32_t ed = ldc(m.tr_ed, (size_t)j);
-      sset((int)(rl(nprv, j) & 0xFFFFu), r_pack(j, 1, ed - 2, ed + ldc(m.tr_init_dist, (size_t)j)));
+      const int32_t ed = rl(t_ed, j);
+      sset((int)(rl(nprv, j) & 0xFFFFu), r_pack(j, 1, ed - 2, ed + ldc(m.tr_pack, (size_t)j * 8 + 5)));
     }
     // pass 4: extend_semaphores (rail_network.py:229-244)
     const uint32_t st4 = tb_state(bits);
@@ -580,7 +636,7 @@ struct WEnv {
       const int j = ctz64(MA);
       MA &= MA - 1ull;
       const int p = (int)(rl(nprv, j) & 0xFFFFu);
-      if (!r_present(sget(p))) sset(p, r_pack(j, 1, t, t + ldc(m.tr_init_dist, (size_t)j)));
+      if (!r_present(sget(p))) sset(p, r_pack(j, 1, t, t + ldc(m.tr_pack, (size_t)j * 8 + 5)));
     }
     // malfunction count (switch_env.py:399-401)
     const uint64_t MF = __ballot(mine && tb_mf(bits) > 0);
@@ -623,17 +679,24 @@ struct WEnv {
     int32_t reward, r_new;
     int next_sw;
     uint64_t slotword;
-    vec_t<double, 4> row;
+    double mq;        // max over the full decision row (successor value for the pending update)
+    double* qp_pend;  // Q cell of the pending update consumed by this decision (or null)
+    double q_pend;    // its value, loaded during the decision
+    uint32_t row_pend;  // key-set row of the pending update
   };
 
   __device__ __forceinline__ void decide(Dec& d, bool greedy) {
+    SFL_PT(t_obs);
     // agent_iter: lowest queued train (switch_env.py:418-421, 616-622)
     const int h = ctz64(q_mask);
     q_mask &= q_mask - 1ull;
     const uint32_t sd = rl(sdec, h);
     const int sw = (int)(sd >> 16);
-    const int np = (int)ldc_u8(m.sw_np, (uint32_t)sw);
-    const int na = (int)ldc_u8(m.sw_na, (uint32_t)sw);
+    const SwRec swr = sw_rec(sw);
+    const vec_t<int32_t, 8> tr = ldcv<vec_t<int32_t, 8>>(m.tr_pack, (size_t)h);
+    const uint64_t slot_v = ld(slotb, slot_ix(sw, h));  // made uniform when needed
+    const int np = swr.np();
+    const int na = swr.na();
     const uint32_t npv = rl(nprv, h);
     const int pin = (int)(npv & 0xFFFFu);
     const int pprev = (int)(npv >> 16);
@@ -642,36 +705,53 @@ struct WEnv {
       lerr |= E_PORT;
       slot = 0;
     }
-    d.slotword = uni(ld(s.slot, ix((size_t)sw * m.T + h)));
     // observe
+    const Blocked bl = blocked_masks(h);
     uint32_t free_bits = 0;
     for (int j = 0; j < np; ++j) {
       const int p = 4 * sw + j;
-      if (!port_blocked(ldc_i16(m.port_nb, (uint32_t)p), p, h)) free_bits |= 1u << j;
+      if (!bl.port(port_nb(p), p)) free_bits |= 1u << j;
     }
     const uint32_t b = rl(bits, h);
     const int32_t p0 = rl(pos, h);
-    const int32_t la = ldc(m.tr_la, (size_t)h);
-    const int32_t dl = now - la + dist(h, p0, (int)tb_dir(b));
-    const int32_t avail = la - ldc(m.tr_ed, (size_t)h);
+    const int32_t ed = tr[0], la = tr[1], k = tr[2];
+    const int32_t dl = now - la + dist(k, p0, (int)tb_dir(b));
+    const int32_t avail = la - ed;
     const uint32_t lvl = dl <= 0 ? 0u : (dl <= avail * 20 ? 1u : 2u);
-    const uint32_t state = ((free_bits * (uint32_t)m.K) + (uint32_t)ldc(m.tr_k, (size_t)h)) * 3u + lvl;
+    const uint32_t state = ((free_bits * (uint32_t)m.K) + (uint32_t)k) * 3u + lvl;
     uint32_t amask = 1u << (na - 1);
     for (int a = 0; a < na - 1; ++a)
-      if ((int)ldc_u8(m.act_src, (uint32_t)(sw * 8 + a)) == slot &&
-          ((free_bits >> ldc_u8(m.act_dst, (uint32_t)(sw * 8 + a))) & 1u))
-        amask |= 1u << a;
-    const int w = (int)ldc_u8(m.q_w, (uint32_t)(4 * sw + slot));
-    const double* rp = qrow(sw, slot, state);
+      if (swr.src(a) == slot && ((free_bits >> swr.dst(a)) & 1u)) amask |= 1u << a;
+    SFL_PACC(0, t_obs);
+    SFL_PT(t_eg);
+    // issue the Q row load and the pending update's Q cell load, then draw while they fly
+    const PortRec prr = port_rec(4 * sw + slot);
+    const int w = prr.q_w();
+    const double* rp = qbase() + prr.q_off() + (size_t)state * (uint32_t)w;
+    vec_t<double, 4> row_v;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) d.row[j] = j < w ? unid(ld(rp, (size_t)j)) : 0.0;
+    for (int j = 0; j < 4; ++j) row_v[j] = j < w ? ld(rp, (size_t)j) : 0.0;
+    d.slotword = uni(slot_v);
+    const uint32_t pend = greedy ? PEND_NONE : slot_pend(d.slotword, epoch);
+    d.qp_pend = nullptr;
+    double q_pend_v = 0.0;
+    if (pend != PEND_NONE) {
+      const int ps = (int)(pend & 0xFFFu);
+      const int pslot = (int)((pend >> 12) & 3u);
+      const uint32_t pstate = (pend >> 14) & 0x3FFFu;
+      const int pj = (int)((pend >> 28) & 3u);
+      const PortRec pr = port_rec(4 * ps + pslot);
+      d.qp_pend = qbase() + pr.q_off() + (size_t)pstate * (uint32_t)pr.q_w() + pj;
+      d.row_pend = pr.row_base() + pstate;
+      q_pend_v = ld(d.qp_pend, 0);
+    }
     const int32_t reward = slot_rew(d.slotword, epoch);
     // epsilon-greedy
     int action = -1;
     bool explore = false;
     if (!greedy) {
       const uint32_t n = cget(sw);
-      const double eps = n < (uint32_t)m.ntab ? ldc(m.eps_tab, (size_t)n) : m.eps0 * pow(m.eps_decay, (double)n);
+      const double eps = n < (uint32_t)m.ntab ? ldc(m.eps_tab, (size_t)n) : m.eps0 * pow_ool(m.eps_decay, (double)n);
       if (pcg_double(rng) < eps) {
         explore = true;
         const uint32_t sub_seed = pcg_bounded(rng, 2147483646u);
@@ -680,75 +760,88 @@ struct WEnv {
         const uint32_t nvalid = (uint32_t)__builtin_popcount(amask);
         const uint32_t pick = pcg_bounded(sub, nvalid - 1u);
         uint32_t mk = amask;
-        for (uint32_t k = 0; k < pick; ++k) mk &= mk - 1u;
+        for (uint32_t kk = 0; kk < pick; ++kk) mk &= mk - 1u;
         action = __builtin_ctz(mk);
       }
     }
-    if (!explore) {
-      if (lane == 0) touch(sw, slot, state);
-      // np.argmax over the full row, falling back to the first allowed maximum (distr_q.py:468-490)
-      int best = 0;
-      double mx = row_val(sw, slot, d.row, 0);
-      for (int a = 1; a < na; ++a) {
-        const double v = row_val(sw, slot, d.row, a);
-        if (v > mx) {
+    vec_t<double, 4> row;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) row[j] = unid(row_v[j]);
+    d.q_pend = unid(q_pend_v);
+    // np.argmax over the full row (first maximum), max(row), and the first allowed maximum
+    // (distr_q.py:449-490), over the compact columns: column c holds full-row action a(c);
+    // every other action of the full row is default_q, the first of them at action mind
+    const uint32_t rd = swr.row_desc(slot);
+    const int mind = (int)((rd >> 16) & 15u);
+    double mx = mind != 15 ? m.default_q : -__builtin_huge_val();
+    int best = mind != 15 ? mind : 99;
+    int arg = -1;
+    double amx = 0.0;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      if (c < w) {
+        const int a = (int)((rd >> (4 * c)) & 15u);
+        const double v = row[c];
+        if (v > mx || (v == mx && a < best)) {
           mx = v;
           best = a;
         }
-      }
-      if ((amask >> best) & 1u) {
-        action = best;
-      } else {
-        double amx = 0.0;
-        for (int a = 0; a < na; ++a) {
-          if (!((amask >> a) & 1u)) continue;
-          const double v = row_val(sw, slot, d.row, a);
-          if (action < 0 || v > amx) {
-            action = a;
+        if ((amask >> a) & 1u) {
+          if (arg < 0 || v > amx || (v == amx && a < arg)) {
+            arg = a;
             amx = v;
           }
         }
       }
     }
+    d.mq = mx;
+    if (!explore) {
+      if (lane == 0) touch_row(prr.row_base() + state);
+      action = ((amask >> best) & 1u) ? best : arg;
+    }
     if (action < 0 || action >= na) lerr |= E_BAD_ACTION;
+    SFL_PACC(1, t_eg);
+    SFL_PT(t_ap);
     // _apply_action
     const int stop = na - 1;
     bool moving = false;
     uint32_t turn = A_FWD;
     int in_p = pin, out_p = pin;
     if (action != stop && (pin >> 2) == sw) {
-      const int src = (int)ldc_u8(m.act_src, (uint32_t)(sw * 8 + action));
+      const int src = swr.src(action);
       if (src == slot) {
         moving = true;
-        turn = ldc_u8(m.act_turn, (uint32_t)(sw * 8 + action));
+        turn = swr.turn(action);
         in_p = 4 * sw + src;
-        out_p = 4 * sw + (int)ldc_u8(m.act_dst, (uint32_t)(sw * 8 + action));
+        out_p = 4 * sw + swr.dst(action);
       }
     }
     int next_sw = sw, target = -1;
     if (moving) {
       // transition_train / transition_semaphore (rail_network.py:246-278, 303-416)
-      target = ldc_i16(m.port_nb, (uint32_t)out_p);
+      const PortRec po = port_rec(out_p);
+      target = po.nb();
+      const PortRec pt = port_rec(target);
       if (tb_state(b) != S_MALF) {
         // free the train's records on the ports of its current and previous switch
         const int x1 = pin >> 2;
         const int x2 = pprev != (int)PORT_NONE ? (pprev >> 2) : -1;
 #pragma unroll
-        for (int k = 0; k < PPL; ++k) {
-          const int x = (k * 64 + lane) >> 2;
-          if ((x == x1 || x == x2) && r_present(sem[k]) && r_owner(sem[k]) == (uint32_t)h) sem[k] = 0u;
+        for (int kk = 0; kk < PPL; ++kk) {
+          const int x = (kk * 64 + lane) >> 2;
+          if ((x == x1 || x == x2) && r_present(sem[kk]) && r_owner(sem[kk]) == (uint32_t)h) sem[kk] = 0u;
         }
       }
-      const int32_t d_ot = ldc_i16(m.port_len, (uint32_t)out_p);
+      const int32_t d_ot = po.len();
       put_keep(out_p, h, 0, 3, 0);
       put_keep(target, h, 1, d_ot + 1, 1);
-      const int u = ldc_i16(m.port_unique, (uint32_t)target);
+      const int u = pt.unique();
       if (u >= 0) {
+        const PortRec pu = port_rec(u);
         if (u != in_p && u != out_p && u != target) put_replace(u, h, 0, d_ot + 1, 0);
         put_replace(u, h, 0, d_ot, -1);
-        const int far = ldc_i16(m.port_nb, (uint32_t)u);
-        if (far != in_p && far != out_p && far != u)
-          put_replace(far, h, 1, d_ot + ldc_i16(m.port_len, (uint32_t)u) + 1, 1);
+        const int far = pu.nb();
+        if (far != in_p && far != out_p && far != u) put_replace(far, h, 1, d_ot + pu.len() + 1, 1);
       }
       if (target != in_p && target != out_p) put_replace(target, h, 0, d_ot + 1, 0);
       tset(sdec, h, (sd & 0xFFFF0000u) | (uint32_t)in_p);
@@ -770,11 +863,10 @@ struct WEnv {
     if (moving) {
       all_blocked = port_blocked(target, out_p, h);
     } else {
-      all_blocked = true;
+      all_blocked = true;  // semaphores unchanged since the observation
       for (int a = 0; a < na - 1; ++a) {
-        if ((int)ldc_u8(m.act_src, (uint32_t)(sw * 8 + a)) != slot) continue;
-        const int o = 4 * sw + (int)ldc_u8(m.act_dst, (uint32_t)(sw * 8 + a));
-        if (!port_blocked(ldc_i16(m.port_nb, (uint32_t)o), o, h)) all_blocked = false;
+        if (swr.src(a) != slot) continue;
+        if ((free_bits >> swr.dst(a)) & 1u) all_blocked = false;
       }
     }
     // reward_func.py:23-78: project the position along the non-STOP plan
@@ -788,7 +880,7 @@ struct WEnv {
       pc = mv.cell;
       pd = mv.dir;
     }
-    const int32_t cur = now - la + dist(h, pc, pd);
+    const int32_t cur = now - la + dist(k, pc, pd);
     const int32_t diff = rl(delay, h) - cur;
     d.r_new = (pl_front(p) == A_STOP && !all_blocked) ? diff - 1300 : diff;
     tset(delay, h, cur);
@@ -797,9 +889,10 @@ struct WEnv {
     d.slot = slot;
     d.state = state;
     d.action = action;
-    d.j = (action == stop) ? (w - 1) : (int)ldc_u8(m.act_j, (uint32_t)(sw * 8 + action));
+    d.j = (action == stop) ? (w - 1) : swr.j(action);
     d.reward = reward;
     d.next_sw = next_sw;
+    SFL_PACC(2, t_ap);
   }
 
   // ---- post-step part of the learn loop (distr_q.py:322-362) -----------------------------------
@@ -808,45 +901,33 @@ struct WEnv {
   __device__ __forceinline__ void post(const Dec& d, bool greedy) {
     const int T = m.T;
     if (greedy) {
-      if (lane == 0) st(s.slot, ix((size_t)d.next_sw * T + d.h), slot_make(PEND_NONE, d.r_new, epoch));
+      if (lane == 0) st(slotb, slot_ix(d.next_sw, d.h), slot_make(PEND_NONE, d.r_new, epoch));
       return;
     }
-    const uint32_t pend = slot_pend(d.slotword, epoch);
-    if (pend != PEND_NONE) {
+    if (d.qp_pend) {
+      const uint32_t pend = slot_pend(d.slotword, epoch);
       const int ps = (int)(pend & 0xFFFu);
-      const int pslot = (int)((pend >> 12) & 3u);
-      const uint32_t pstate = (pend >> 14) & 0x3FFFu;
-      const int pj = (int)((pend >> 28) & 3u);
       const double lr = lr_of(cget(ps));
-      double* qp = qrow(ps, pslot, pstate) + pj;
-      const double qv = unid(ld(qp, 0));
       const double r = (double)d.reward;
       double nv;
       if (d.sw != ps) {
-        // max(row) over the full, unmasked successor row (distr_q.py:449-466)
-        const int na = (int)ldc_u8(m.sw_na, (uint32_t)d.sw);
-        double mq = row_val(d.sw, d.slot, d.row, 0);
-        for (int a = 1; a < na; ++a) {
-          const double v = row_val(d.sw, d.slot, d.row, a);
-          mq = v > mq ? v : mq;
-        }
-        const double a1 = (1.0 - lr) * qv;
-        const double b1 = lr * (r + m.gamma * mq);
+        const double a1 = (1.0 - lr) * d.q_pend;
+        const double b1 = lr * (r + m.gamma * d.mq);
         nv = a1 + b1;
       } else {
-        const double a1 = (1.0 - lr) * qv;
+        const double a1 = (1.0 - lr) * d.q_pend;
         const double b1 = lr * r;
         nv = a1 + b1;
       }
       if (lane == 0) {
-        st(qp, 0, nv);
-        touch(ps, pslot, pstate);
-        if (d.sw != ps) touch(d.sw, d.slot, d.state);
+        st(d.qp_pend, 0, nv);
+        touch_row(d.row_pend);
+        if (d.sw != ps) touch_row(port_rec(4 * d.sw + d.slot).row_base() + d.state);
       }
     }
     if (lane == 0) {
-      st(s.slot, ix((size_t)d.sw * T + d.h), slot_make(PEND_NONE, slot_rew(d.slotword, epoch), epoch));
-      st(s.slot, ix((size_t)d.next_sw * T + d.h),
+      st(slotb, slot_ix(d.sw, d.h), slot_make(PEND_NONE, slot_rew(d.slotword, epoch), epoch));
+      st(slotb, slot_ix(d.next_sw, d.h),
          slot_make(pend_make((uint32_t)d.sw, (uint32_t)d.slot, d.state, (uint32_t)d.j), d.r_new, epoch));
     }
     // destination bonus for newly arrived trains (distr_q.py:344-356); lanes take switches.
@@ -860,7 +941,7 @@ struct WEnv {
       for (int base = 0; base < m.S; base += 64) {
         const int sw2 = base + lane;
         const bool valid = sw2 < m.S;
-        const uint64_t slw = valid ? ld(s.slot, ix((size_t)sw2 * T + tr)) : 0ull;
+        const uint64_t slw = valid ? ld(slotb, slot_ix(sw2, tr)) : 0ull;
         const uint32_t pe = valid ? slot_pend(slw, epoch) : PEND_NONE;
         const int ps = pe == PEND_NONE ? 0 : (int)(pe & 0xFFFu);
         const uint32_t n = cget_var(ps);  // all lanes active: a bpermute reads 0 from inactive lanes
@@ -869,14 +950,13 @@ struct WEnv {
         const uint32_t pstate = (pe >> 14) & 0x3FFFu;
         const int pj = (int)((pe >> 28) & 3u);
         const double lr = lr_of_var(n);
-        const int g = 4 * ps + pslot;
-        double* qp = s.q + (size_t)e * m.q_per_env + ld(m.q_off, (size_t)g) + (size_t)pstate * ld(m.q_w, (size_t)g) + pj;
+        const u4 pr = ld((const u4*)m.port_pack, (size_t)(4 * ps + pslot));
+        double* qp = qbase() + pr[3] + (size_t)pstate * (pr[1] >> 16) + pj;
         const double a1 = (1.0 - lr) * ld(qp, 0);
         const double b1 = lr * (1000.0 + m.gamma * 0.0);
         st(qp, 0, a1 + b1);
-        const uint32_t row = ld(m.row_base, (size_t)g) + pstate;
-        atomicOr(&s.touched[(size_t)e * m.touched_words + (row >> 5)], 1u << (row & 31u));
-        st(s.slot, ix((size_t)sw2 * T + tr), slot_make(PEND_NONE, slot_rew(slw, epoch), epoch));
+        touch_row(pr[2] + pstate);
+        st(slotb, slot_ix(sw2, tr), slot_make(PEND_NONE, slot_rew(slw, epoch), epoch));
       }
     }
     cset(d.sw, cget(d.sw) + 1u);
@@ -906,13 +986,19 @@ __device__ void run(const SflMap& m, const SflState& s, const SflCtl& c) {
   v.load();
   int32_t phase = uni(ld(s.phase, e));
   int32_t ep_t = uni(ld(s.ep_t, e)), n_test = uni(ld(s.n_test, e));
-  uint64_t dec = 0, ticks = 0, abytes = 0;
+  uint32_t ticks = 0, abytes = 0;
   typename V::Dec d;
   d.sw = d.h = d.slot = d.action = d.j = d.reward = d.r_new = d.next_sw = 0;
   d.state = 0;
   d.slotword = 0;
-  d.row = 0.0;
+  d.mq = d.q_pend = 0.0;
+  d.qp_pend = nullptr;
+  d.row_pend = 0;
   const bool test_mode = c.mode == 1;
+#ifdef SFL_PROFILE
+  uint64_t prof[5] = {0, 0, 0, 0, 0};
+  const uint64_t t_begin = (uint64_t)__builtin_amdgcn_s_memtime();
+#endif
   while (true) {
     if (phase == PH_RESET) {
       // learn: optional greedy round before episode t (distr_q.py:278-281)
@@ -924,11 +1010,15 @@ __device__ void run(const SflMap& m, const SflState& s, const SflCtl& c) {
         if (c.exploit_freq > 0 && (ep_t + 1) % c.exploit_freq == 0 && !(v.flags & F_EXPLOIT_DONE)) v.flags |= F_GREEDY;
         else v.flags &= ~F_GREEDY;
       }
+      SFL_PT(t0);
       v.reset();
+      SFL_PACC(0, t0);
       phase = PH_TICK;
     } else if (phase == PH_TICK) {
-      abytes += 36ull * (uint64_t)(m.T - popc64(v.arr_mask));
+      abytes += 36u * (uint32_t)(m.T - popc64(v.arr_mask));
+      SFL_PT(t0);
       v.tick();
+      SFL_PACC(1, t0);
       ticks++;
       if (v.flags & F_TERM) phase = (v.flags & F_INFLIGHT) ? PH_POST : PH_END;
       else if (v.q_mask) phase = (v.flags & F_INFLIGHT) ? PH_POST : PH_DECIDE;
@@ -936,14 +1026,19 @@ __device__ void run(const SflMap& m, const SflState& s, const SflCtl& c) {
       bool post_now = phase == PH_POST;
       const bool greedy = (v.flags & F_GREEDY) != 0;
       if (phase == PH_DECIDE) {
+        SFL_PT(t0);
         v.decide(d, greedy);
-        abytes += 220ull + 48ull * ldc_u8(m.sw_np, (uint32_t)d.sw) + 8ull * ldc_u8(m.sw_na, (uint32_t)d.sw);
+        SFL_PACC(2, t0);
+        const uint32_t w0 = ldc(m.sw_pack, (size_t)d.sw * 8);
+        abytes += 220u + 48u * (w0 & 15u) + 8u * ((w0 >> 4) & 15u);
         v.flags |= F_INFLIGHT;
         if (!v.q_mask) phase = PH_TICK;  // ticks happen between the step and the update
         else post_now = true;
       }
       if (post_now) {
+        SFL_PT(t0);
         v.post(d, greedy);
+        SFL_PACC(3, t0);
         if (c.trace && (int32_t)e == c.trace_env) {
           const uint64_t cs = v.sem_checksum();
           if (lane == 0) {
@@ -962,12 +1057,11 @@ __device__ void run(const SflMap& m, const SflState& s, const SflCtl& c) {
         v.flags &= ~F_INFLIGHT;
         v.cum += (double)d.reward;
         v.ep_dec += 1;
-        v.dec_total += 1;
+        v.n_dec += 1;
         v.step_ctr += 1;
         if (v.step_ctr > m.max_steps) v.flags |= F_TRUNC;
-        dec++;
         phase = (v.flags & (F_TERM | F_TRUNC)) ? PH_END : PH_DECIDE;
-        if (c.dec_budget > 0 && (int64_t)dec >= c.dec_budget) break;
+        if (c.dec_budget > 0 && (int64_t)v.n_dec >= c.dec_budget) break;
       }
     } else {  // PH_END
       const int arrived = popc64(v.arr_mask);
@@ -1001,12 +1095,19 @@ __device__ void run(const SflMap& m, const SflState& s, const SflCtl& c) {
     }
   }
   v.store(phase);
+#ifdef SFL_PROFILE
+  prof[4] = (uint64_t)__builtin_amdgcn_s_memtime() - t_begin;
+  if (lane == 0) {
+    for (int k = 0; k < 5; ++k) atomicAdd(&g_prof[k], (unsigned long long)prof[k]);
+    for (int k = 0; k < 3; ++k) atomicAdd(&g_prof[5 + k], (unsigned long long)v.prof[k]);
+  }
+#endif
   if (lane == 0) {
     st(s.ep_t, e, ep_t);
     st(s.n_test, e, n_test);
-    if (c.launch_dec) st(c.launch_dec, e, dec);
-    if (c.launch_ticks) st(c.launch_ticks, e, ticks);
-    if (c.launch_bytes) st(c.launch_bytes, e, abytes);
+    if (c.launch_dec) st(c.launch_dec, e, (uint64_t)v.n_dec);
+    if (c.launch_ticks) st(c.launch_ticks, e, (uint64_t)ticks);
+    if (c.launch_bytes) st(c.launch_bytes, e, (uint64_t)abytes);
   }
 }
 
