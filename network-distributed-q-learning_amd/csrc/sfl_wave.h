@@ -140,8 +140,11 @@ struct WEnv {
   // timetable constants of train `lane` (tr_pack)
   int32_t t_ed, t_target, t_init_cell;
   uint32_t t_init;  // init dir | init port << 16
-  vec_t<uint32_t, PPL> sem;
-  vec_t<uint32_t, SPL> cnt;
+  // this env's semaphore records and switch counters in LDS (one region per wave):
+  // uniform reads are broadcast ds_reads, writes one lane's ds_write, and the lane-parallel
+  // scans read entries k*64 + lane (conflict-free)
+  uint32_t* lsem;  // [64*PPL]
+  uint32_t* lcnt;  // [64*SPL]
   uint32_t lerr;  // error bits seen by this lane (OR-reduced on store)
   // this env's blocks: Q-table, key-set bitmap, (switch, train) slots (env-major [T][S] here,
   // so one env's slots are contiguous and a flush over switches is one coalesced access)
@@ -161,8 +164,8 @@ struct WEnv {
   uint64_t prof[3] = {0, 0, 0};  // decide: observe, epsilon-greedy, apply
 #endif
 
-  __device__ WEnv(const SflMap& m_, const SflState& s_, uint32_t e_, int lane_)
-      : m(m_), s(s_), e(e_), E(s_.E), lane(lane_), mine(lane_ < m_.T) {
+  __device__ WEnv(const SflMap& m_, const SflState& s_, uint32_t e_, int lane_, uint32_t* lds)
+      : m(m_), s(s_), e(e_), E(s_.E), lane(lane_), mine(lane_ < m_.T), lsem(lds), lcnt(lds + 64 * PPL) {
     qb = s.q + (size_t)e * m.q_per_env;
     touchb = s.touched + (size_t)e * m.touched_words;
     slotb = s.slot + (size_t)e * (uint32_t)(m.S * m.T);
@@ -172,35 +175,16 @@ struct WEnv {
   __device__ __forceinline__ size_t ix(size_t i) const { return i * (size_t)E + e; }
 
   // ---- cross-lane access (index wave-uniform) -------------------------------------
-  __device__ __forceinline__ uint32_t sget(int p) const {
-    uint32_t r = rl(sem[0], p & 63);
-#pragma unroll
-    for (int i = 1; i < PPL; ++i) r = (i == (p >> 6)) ? rl(sem[i], p & 63) : r;
-    return r;
-  }
+  __device__ __forceinline__ uint32_t sget(int p) const { return lsem[p]; }
   __device__ __forceinline__ void sset(int p, uint32_t r) {
-    const bool me = lane == (p & 63);
-#pragma unroll
-    for (int i = 0; i < PPL; ++i) sem[i] = (me && i == (p >> 6)) ? r : sem[i];
+    if (lane == 0) lsem[p] = r;
   }
-  __device__ __forceinline__ uint32_t cget(int sw) const { return rl(cnt[sw >> 6], sw & 63); }
+  __device__ __forceinline__ uint32_t& sem(int k) const { return lsem[k * 64 + lane]; }  // lane-parallel
+  __device__ __forceinline__ uint32_t cget(int sw) const { return lcnt[sw]; }
   __device__ __forceinline__ void cset(int sw, uint32_t v) {
-    const int k = sw >> 6;
-    const bool me = lane == (sw & 63);
-#pragma unroll
-    for (int i = 0; i < SPL; ++i)
-      if (i == k) cnt[i] = me ? v : cnt[i];
+    if (lane == 0) lcnt[sw] = v;
   }
-  // counter of a per-lane switch index (flush): bpermute per register; call with all lanes active
-  __device__ __forceinline__ uint32_t cget_var(int sw) const {
-    uint32_t r = 0;
-#pragma unroll
-    for (int i = 0; i < SPL; ++i) {
-      const uint32_t v = (uint32_t)__shfl((int)cnt[i], sw & 63, 64);
-      r = (i == (sw >> 6)) ? v : r;
-    }
-    return r;
-  }
+  __device__ __forceinline__ uint32_t cget_var(int sw) const { return lcnt[sw]; }  // per-lane index
   template <class T>
   __device__ __forceinline__ void tset(T& x, int h, T v) {
     x = (lane == h) ? v : x;
@@ -280,7 +264,7 @@ struct WEnv {
     Blocked bl;
 #pragma unroll
     for (int k = 0; k < PPL; ++k) {
-      const uint32_t r = sem[k];
+      const uint32_t r = sem(k);
       const uint32_t ow = r_owner(r);
       const bool live = r_present(r) && ow != (uint32_t)h && r_t0(r) <= now && now <= r_t1(r);
       const bool mf = (malf >> ow) & 1ull;
@@ -338,12 +322,12 @@ struct WEnv {
 #pragma unroll
     for (int k = 0; k < PPL; ++k) {
       const int p = k * 64 + lane;
-      sem[k] = p < m.NP ? r_from64(ld(s.sem, ix(p))) : 0u;
+      sem(k) = p < m.NP ? r_from64(ld(s.sem, ix(p))) : 0u;
     }
 #pragma unroll
     for (int k = 0; k < SPL; ++k) {
       const int sw = k * 64 + lane;
-      cnt[k] = sw < m.S ? ld(s.counts, ix(sw)) : 0u;
+      lcnt[k * 64 + lane] = sw < m.S ? ld(s.counts, ix(sw)) : 0u;
     }
     now = uni(ld(s.elapsed, e));
     flags = uni(ld(s.eflags, e));
@@ -385,12 +369,12 @@ struct WEnv {
 #pragma unroll
     for (int k = 0; k < PPL; ++k) {
       const int p = k * 64 + lane;
-      if (p < m.NP) st(s.sem, ix(p), r_to64(sem[k]));
+      if (p < m.NP) st(s.sem, ix(p), r_to64(sem(k)));
     }
 #pragma unroll
     for (int k = 0; k < SPL; ++k) {
       const int sw = k * 64 + lane;
-      if (sw < m.S) st(s.counts, ix(sw), cnt[k]);
+      if (sw < m.S) st(s.counts, ix(sw), lcnt[k * 64 + lane]);
     }
     uint32_t err = 0;
 #pragma unroll
@@ -432,7 +416,8 @@ struct WEnv {
       nprv = (nprv & 0xFFFF0000u) | (t_init >> 16);
       delay = ld(m.tr_pack, (size_t)lane * 8 + 6);
     }
-    sem = 0u;
+#pragma unroll
+    for (int k = 0; k < PPL; ++k) sem(k) = 0u;
     for (int h = 0; h < m.T; ++h) {
       const vec_t<int32_t, 8> tr = ldcv<vec_t<int32_t, 8>>(m.tr_pack, (size_t)h);
       sset((int)((uint32_t)tr[7] >> 16), r_pack(h, 1, tr[0] - 2, tr[0] + tr[5]));
@@ -611,7 +596,7 @@ struct WEnv {
     if (DONE) {
 #pragma unroll
       for (int k = 0; k < PPL; ++k)
-        if (r_present(sem[k]) && ((DONE >> r_owner(sem[k])) & 1ull)) sem[k] = 0u;
+        if (r_present(sem(k)) && ((DONE >> r_owner(sem(k))) & 1ull)) sem(k) = 0u;
     }
     // departure semaphores, in handle order (switch_env.py:379-384)
     uint64_t D = __ballot(dep);
@@ -627,8 +612,8 @@ struct WEnv {
     if (SM) {
 #pragma unroll
       for (int k = 0; k < PPL; ++k) {
-        const uint32_t r = sem[k];
-        if (r_present(r) && ((SM >> r_owner(r)) & 1ull)) sem[k] = r_pack(r_owner(r), r_in(r), t, t + (r_t1(r) - r_t0(r)));
+        const uint32_t r = sem(k);
+        if (r_present(r) && ((SM >> r_owner(r)) & 1ull)) sem(k) = r_pack(r_owner(r), r_in(r), t, t + (r_t1(r) - r_t0(r)));
       }
     }
     uint64_t MA = __ballot(mine && st4 == S_MALF);
@@ -829,7 +814,8 @@ struct WEnv {
 #pragma unroll
         for (int kk = 0; kk < PPL; ++kk) {
           const int x = (kk * 64 + lane) >> 2;
-          if ((x == x1 || x == x2) && r_present(sem[kk]) && r_owner(sem[kk]) == (uint32_t)h) sem[kk] = 0u;
+          const uint32_t r = sem(kk);
+          if ((x == x1 || x == x2) && r_present(r) && r_owner(r) == (uint32_t)h) sem(kk) = 0u;
         }
       }
       const int32_t d_ot = po.len();
@@ -968,7 +954,7 @@ struct WEnv {
 #pragma unroll
     for (int k = 0; k < PPL; ++k) {
       const int p = k * 64 + lane;
-      if (p < m.NP && r_present(sem[k])) c0 += mix64(((uint64_t)p << 42) ^ r_to64(sem[k]));
+      if (p < m.NP && r_present(sem(k))) c0 += mix64(((uint64_t)p << 42) ^ r_to64(sem(k)));
     }
     for (int off = 1; off < 64; off <<= 1) c0 += (uint64_t)__shfl_xor((long long)c0, off, 64);
     return c0;
@@ -982,7 +968,8 @@ __device__ void run(const SflMap& m, const SflState& s, const SflCtl& c) {
   const int lane = (int)__lane_id();
   const uint32_t e = uni((uint32_t)((blockIdx.x * blockDim.x + threadIdx.x) >> 6));
   if (e >= s.E) return;
-  V v(m, s, e, lane);
+  __shared__ uint32_t lds[4 * 64 * (PPL + SPL)];
+  V v(m, s, e, lane, lds + (threadIdx.x >> 6) * 64 * (PPL + SPL));
   v.load();
   int32_t phase = uni(ld(s.phase, e));
   int32_t ep_t = uni(ld(s.ep_t, e)), n_test = uni(ld(s.n_test, e));
