@@ -45,7 +45,7 @@ constexpr uint32_t PEND_NONE = 0xFFFFFFFFu;
 constexpr uint16_t PORT_NONE = 0xFFFFu;
 
 struct SflMap {
-  int32_t H, W, S, T, K, NP;
+  int32_t H, W, S, T, K, NP, HW;
   int32_t max_episode_steps, mf_min, mf_max, ntab;
   double mf_rate, gamma, eps0, eps_decay, lr0, lr_decay, default_q;
   int64_t max_steps;
@@ -82,7 +82,8 @@ struct SflMap {
   const double* eps_tab;
   const double* lr_tab;
   // packed copies for the one-env-per-wave kernel (sfl_wave.h), built at create time
-  const uint32_t* sw_pack;    // [S][8]: np | na<<4; src/dst 2b per action; turn/j 2b; q_w 4b per slot; row map per slot
+  const uint32_t* sw_pack;    // [S][16]: np | na<<4; src/dst 2b per action; turn/j 2b; q_w 4b per slot; row map per slot;
+                              // neighbour port of ports 0-3 (16 b each) in words 8-9; 10-15 spare
   const uint32_t* port_pack;  // [NP][4]: nb | len<<16; unique | q_w<<16; row_base; q_off
   const uint32_t* move_tab;   // [H*W][4 dir][4 action&3]: check_action result (see move_pack)
   const int32_t* tr_pack;     // [T][8]: ed, la, k, target, init_cell, init_dist, init_delay, init_dir | init_port<<16

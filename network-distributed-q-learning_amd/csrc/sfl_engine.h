@@ -113,6 +113,7 @@ int create(const sfl_map_desc* md, const sfl_hparams* hp, uint32_t n_envs, const
   const size_t HW = (size_t)md->H * md->W, NP = (size_t)md->S * 4, S = md->S, T = md->T;
   m.H = md->H;
   m.W = md->W;
+  m.HW = md->H * md->W;
   m.S = md->S;
   m.T = md->T;
   m.K = md->K;
@@ -165,11 +166,11 @@ int create(const sfl_map_desc* md, const sfl_hparams* hp, uint32_t n_envs, const
   {
     // packed tables for the one-env-per-wave kernel: one scalar load per switch / port / train,
     // and check_action as a table lookup
-    std::vector<uint32_t> swp(S * 8, 0), pp(NP * 4, 0), mv(HW * 16, 0);
+    std::vector<uint32_t> swp(S * 16, 0), pp(NP * 4, 0), mv(HW * 16, 0);
     std::vector<int32_t> trp(T * 8, 0);
     bool pack_ok = true;
     for (size_t sw = 0; sw < S; ++sw) {
-      uint32_t* w = &swp[sw * 8];
+      uint32_t* w = &swp[sw * 16];
       const int na = md->sw_na[sw];
       w[0] = (uint32_t)md->sw_np[sw] | ((uint32_t)na << 4);
       for (int a = 0; a < 8 && a < na - 1; ++a) {  // routes (STOP = action na-1 has no entry)
@@ -199,6 +200,8 @@ int create(const sfl_map_desc* md, const sfl_hparams* hp, uint32_t n_envs, const
         rd |= mind << 16;
         if (rd >> 31) pack_ok = false;
         w[4 + sl] = rd;
+        // neighbour port of each port (observer lanes)
+        w[8 + (sl >> 1)] |= (uint32_t)(uint16_t)md->port_nb[sw * 4 + sl] << (16 * (sl & 1));
       }
     }
     for (size_t p = 0; p < NP; ++p) {

@@ -99,6 +99,19 @@ __device__ __attribute__((noinline)) double pow_ool(double base, double n) { ret
 __device__ __forceinline__ int ctz64(uint64_t x) { return __builtin_ctzll(x); }
 __device__ __forceinline__ int popc64(uint64_t x) { return __builtin_popcountll(x); }
 
+// max over each quad of lanes (DPP quad permutes; the result is valid in every lane of the quad)
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double x) {
+  const long long u = __double_as_longlong(x);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)u, CTRL, 0xF, 0xF, false);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(u >> 32), CTRL, 0xF, 0xF, false);
+  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+__device__ __forceinline__ double quad_max(double x) {
+  x = fmax(x, dpp_f64<0xB1>(x));  // quad_perm [1,0,3,2]
+  return fmax(x, dpp_f64<0x4E>(x));  // quad_perm [2,3,0,1]
+}
+
 // packed switch record (SflMap::sw_pack), wave-uniform
 struct SwRec {
   u8 w;
@@ -192,7 +205,11 @@ struct WEnv {
   __device__ __forceinline__ uint32_t state_of(int h) const { return tb_state(rl(bits, h)); }
 
   // ---- map records --------------------------------------------------------------------
-  __device__ __forceinline__ SwRec sw_rec(int sw) const { return SwRec{ldcv<u8>(m.sw_pack, (size_t)sw)}; }
+  __device__ __forceinline__ SwRec sw_rec(int sw) const { return SwRec{ldcv<u8>(m.sw_pack, (size_t)sw * 2u)}; }
+  // neighbour ports of the switch's ports 0-3 (16 bits each)
+  __device__ __forceinline__ vec_t<uint32_t, 2> sw_nb(int sw) const {
+    return ldcv<vec_t<uint32_t, 2>>(m.sw_pack, (size_t)sw * 8u + 4u);
+  }
   __device__ __forceinline__ PortRec port_rec(int p) const { return PortRec{ldcv<u4>(m.port_pack, (size_t)p)}; }
   __device__ __forceinline__ int port_nb(int p) const { return (int)(int16_t)(ldc(m.port_pack, (size_t)p * 4) & 0xFFFFu); }
   struct Move {
@@ -210,7 +227,7 @@ struct WEnv {
   // flatland-lite check_action_on_agent as a table lookup; U: wave-uniform arguments (scalar load)
   template <bool U>
   __device__ __forceinline__ Move check_action(uint32_t a, int cell, int dir) const {
-    const size_t i = ((size_t)cell * 4 + (size_t)dir) * 4 + (a & 3u);
+    const uint32_t i = ((uint32_t)cell * 4u + (uint32_t)dir) * 4u + (a & 3u);
     return unpack_move(U ? ldc(m.move_tab, i) : ld(m.move_tab, i));
   }
   template <bool U>
@@ -224,7 +241,7 @@ struct WEnv {
       lerr |= E_INF_DIST;
       return 0;
     }
-    const int32_t d = ldc(m.dist, (((size_t)k * m.H * m.W) + (size_t)cell) * 4 + dir);
+    const int32_t d = ldc(m.dist, ((uint32_t)k * (uint32_t)m.HW + (uint32_t)cell) * 4u + (uint32_t)dir);
     if (d >= DIST_INF) lerr |= E_INF_DIST;
     return d;
   }
@@ -243,6 +260,16 @@ struct WEnv {
       if (state_of((int)r_owner(r)) == S_MALF) return true;
     }
     return false;
+  }
+  // does record r block a train h entering through its port (io = 0: the next port) or leaving
+  // through it (io = 1: the out port)?  0/1 in integer VALU: present, owned by another train,
+  // inside its [t0, t1] window, and of the opposite direction or owned by a malfunctioning train
+  __device__ __forceinline__ uint32_t rec_blocks(uint32_t r, uint32_t h, uint64_t malf, uint32_t io) const {
+    const uint32_t ow = r_owner(r);
+    const uint32_t win = (uint32_t)(~((now - r_t0(r)) | (r_t1(r) - now))) >> 31;
+    const uint32_t other = ((ow ^ h) + 0xFFu) >> 8;
+    const uint32_t mf = (uint32_t)(malf >> ow) & 1u;
+    return (r >> 31) & win & other & ((r_in(r) ^ io ^ 1u) | mf);
   }
   // check_port_blocked for every record at once: lane-parallel over each lane's records, one
   // ballot per register.  bn: the record blocks a train entering through it (next port),
@@ -690,13 +717,18 @@ struct WEnv {
       lerr |= E_PORT;
       slot = 0;
     }
-    // observe
-    const Blocked bl = blocked_masks(h);
-    uint32_t free_bits = 0;
-    for (int j = 0; j < np; ++j) {
-      const int p = 4 * sw + j;
-      if (!bl.port(port_nb(p), p)) free_bits |= 1u << j;
-    }
+    // observe: lane j < np evaluates check_port_blocked(next_port(p_j), p_j) for port j of the
+    // switch (observer.py:44-151, 269-283), branch-free integer VALU, then one ballot; lane a
+    // evaluates get_action_mask for route a (switch_agents.py:104-134)
+    const vec_t<uint32_t, 2> nbw = sw_nb(sw);
+    const int pj = 4 * sw + (lane & 3);
+    const uint32_t nbl = ((lane & 2) ? nbw[1] : nbw[0]) >> ((lane & 1) * 16);
+    const bool pvalid = lane < np;
+    const int nbj = pvalid ? (int)(nbl & 0xFFFFu) : pj;
+    const uint64_t malf = __ballot(mine && tb_state(bits) == S_MALF);
+    const uint32_t rn = lsem[nbj], ro = lsem[pj];
+    const uint32_t blk = rec_blocks(rn, (uint32_t)h, malf, 0u) | rec_blocks(ro, (uint32_t)h, malf, 1u);
+    const uint32_t free_bits = (uint32_t)__ballot(pvalid && blk == 0u) & 15u;
     const uint32_t b = rl(bits, h);
     const int32_t p0 = rl(pos, h);
     const int32_t ed = tr[0], la = tr[1], k = tr[2];
@@ -704,18 +736,20 @@ struct WEnv {
     const int32_t avail = la - ed;
     const uint32_t lvl = dl <= 0 ? 0u : (dl <= avail * 20 ? 1u : 2u);
     const uint32_t state = ((free_bits * (uint32_t)m.K) + (uint32_t)k) * 3u + lvl;
-    uint32_t amask = 1u << (na - 1);
-    for (int a = 0; a < na - 1; ++a)
-      if (swr.src(a) == slot && ((free_bits >> swr.dst(a)) & 1u)) amask |= 1u << a;
+    const uint32_t la7 = (uint32_t)lane & 7u;
+    const uint32_t srca = (swr.w[1] >> (2u * la7)) & 3u, dsta = (swr.w[1] >> (16u + 2u * la7)) & 3u;
+    const uint32_t amask =
+        ((uint32_t)__ballot(lane < na - 1 && srca == (uint32_t)slot && ((free_bits >> dsta) & 1u)) & 0xFFu) |
+        (1u << (na - 1));
     SFL_PACC(0, t_obs);
     SFL_PT(t_eg);
     // issue the Q row load and the pending update's Q cell load, then draw while they fly
     const PortRec prr = port_rec(4 * sw + slot);
     const int w = prr.q_w();
-    const double* rp = qbase() + prr.q_off() + (size_t)state * (uint32_t)w;
-    vec_t<double, 4> row_v;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) row_v[j] = j < w ? ld(rp, (size_t)j) : 0.0;
+    const double* rp = qbase() + (prr.q_off() + state * (uint32_t)w);
+    // lane c < w holds compact column c of the row
+    const bool colv = lane < w;
+    const double v_c = ld(rp, (size_t)(colv ? lane : 0));
     d.slotword = uni(slot_v);
     const uint32_t pend = greedy ? PEND_NONE : slot_pend(d.slotword, epoch);
     d.qp_pend = nullptr;
@@ -749,36 +783,29 @@ struct WEnv {
         action = __builtin_ctz(mk);
       }
     }
-    vec_t<double, 4> row;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) row[j] = unid(row_v[j]);
     d.q_pend = unid(q_pend_v);
     // np.argmax over the full row (first maximum), max(row), and the first allowed maximum
-    // (distr_q.py:449-490), over the compact columns: column c holds full-row action a(c);
-    // every other action of the full row is default_q, the first of them at action mind
+    // (distr_q.py:449-490), over the compact columns held by lanes 0..w-1 (column order = action
+    // order, so the lowest lane among equal values is the first index): column c holds full-row
+    // action a(c); every other action of the full row is default_q, the first of them at mind
     const uint32_t rd = swr.row_desc(slot);
     const int mind = (int)((rd >> 16) & 15u);
-    double mx = mind != 15 ? m.default_q : -__builtin_huge_val();
-    int best = mind != 15 ? mind : 99;
-    int arg = -1;
-    double amx = 0.0;
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      if (c < w) {
-        const int a = (int)((rd >> (4 * c)) & 15u);
-        const double v = row[c];
-        if (v > mx || (v == mx && a < best)) {
-          mx = v;
-          best = a;
-        }
-        if ((amask >> a) & 1u) {
-          if (arg < 0 || v > amx || (v == amx && a < arg)) {
-            arg = a;
-            amx = v;
-          }
-        }
-      }
+    const uint32_t a_c = (rd >> (4u * ((uint32_t)lane & 3u))) & 15u;
+    const double NEG = -__builtin_huge_val();
+    const double vq = colv ? v_c : NEG;
+    const double vm = (colv && ((amask >> a_c) & 1u)) ? v_c : NEG;
+    const double mq4 = quad_max(vq), am4 = quad_max(vm);
+    const double mqu = unid(mq4), amu = unid(am4);
+    const int cb = ctz64(__ballot(colv && v_c == mqu));
+    const int ca = ctz64(__ballot(vm == amu && colv && ((amask >> a_c) & 1u)));
+    double mx = __longlong_as_double(((long long)(uint32_t)__builtin_amdgcn_readlane((int)(__double_as_longlong(v_c) >> 32), cb) << 32) |
+                                     (long long)(uint32_t)__builtin_amdgcn_readlane((int)__double_as_longlong(v_c), cb));
+    int best = (int)((rd >> (4 * cb)) & 15u);
+    if (mind != 15 && (m.default_q > mx || (m.default_q == mx && mind < best))) {
+      mx = m.default_q;
+      best = mind;
     }
+    const int arg = (int)((rd >> (4 * ca)) & 15u);
     d.mq = mx;
     if (!explore) {
       if (lane == 0) touch_row(prr.row_base() + state);
@@ -1016,7 +1043,7 @@ __device__ void run(const SflMap& m, const SflState& s, const SflCtl& c) {
         SFL_PT(t0);
         v.decide(d, greedy);
         SFL_PACC(2, t0);
-        const uint32_t w0 = ldc(m.sw_pack, (size_t)d.sw * 8);
+        const uint32_t w0 = ldc(m.sw_pack, (size_t)d.sw * 16);
         abytes += 220u + 48u * (w0 & 15u) + 8u * ((w0 >> 4) & 15u);
         v.flags |= F_INFLIGHT;
         if (!v.q_mask) phase = PH_TICK;  // ticks happen between the step and the update
