@@ -25,13 +25,23 @@ namespace wave {
 #ifdef SFL_PROFILE
 // tuning builds only: wall cycles per phase summed over waves (reset, tick, decide, post, total,
 // decide = observe + egreedy + apply)
-__device__ unsigned long long g_prof[8];
+__device__ unsigned long long g_prof[16];
+#define SFL_PCNT(k) (prof[k] += 1)
 #define SFL_PT(var) const uint64_t var = (uint64_t)__builtin_amdgcn_s_memtime()
 #define SFL_PACC(k, t0) prof[k] += (uint64_t)__builtin_amdgcn_s_memtime() - (t0)
 #else
 #define SFL_PT(var)
 #define SFL_PACC(k, t0)
+#define SFL_PCNT(k)
 #endif
+
+constexpr uint32_t PF_NONE = 0xFFFFFFFFu;
+// batch-prefetch record per train (doubles): row 0-3, pending cell 4, slot word 5, then int32 words
+// from PF_I: distance-map value at the train's cell (observation), at its projected cell if it
+// stops (reward of STOP), and if it moves with final rail action 0..3 (reward of a route)
+constexpr int PF_W = 10, PF_I = 12;
+constexpr int EPS_WIN = 1024;  // epsilon table entries kept in LDS
+constexpr int32_t PF_OFFGRID = (int32_t)0x80000000;  // projection left the grid
 
 #define SFL_AS_G __attribute__((address_space(1)))
 #define SFL_AS_C __attribute__((address_space(4)))
@@ -158,6 +168,13 @@ struct WEnv {
   // scans read entries k*64 + lane (conflict-free)
   uint32_t* lsem;  // [64*PPL]
   uint32_t* lcnt;  // [64*SPL]
+  // batch prefetch (see prefetch()): per queued train (lane), the staged Q row, the pending
+  // update's Q cell value and the slot word in LDS, and the staged offsets in VGPRs
+  double* lpf;       // [64][PF_W]: row columns 0-3 | pending cell value | slot word (as bits) | int32 distances (PF_D0..)
+  uint32_t pf_roff;  // offset of the staged row in the env's Q block (PF_NONE: none)
+  uint32_t pf_qoff;  // offset of the staged pending cell (PF_NONE: none)
+  bool pf_ok;        // uniform: this batch has been prefetched
+  const double* leps;  // LDS copy of eps_tab[0, EPS_WIN) (shared by the block)
   uint32_t lerr;  // error bits seen by this lane (OR-reduced on store)
   // this env's blocks: Q-table, key-set bitmap, (switch, train) slots (env-major [T][S] here,
   // so one env's slots are contiguous and a flush over switches is one coalesced access)
@@ -174,12 +191,14 @@ struct WEnv {
   int32_t step_ctr;
   uint32_t n_dec;  // decisions in this launch (dec_total += n_dec on store)
 #ifdef SFL_PROFILE
-  uint64_t prof[3] = {0, 0, 0};  // decide: observe, epsilon-greedy, apply
+  uint64_t prof[9] = {};  // decide: observe, epsilon-greedy, apply; events: prefetch, row hit/miss, pend hit/miss, decisions
 #endif
 
-  __device__ WEnv(const SflMap& m_, const SflState& s_, uint32_t e_, int lane_, uint32_t* lds)
-      : m(m_), s(s_), e(e_), E(s_.E), lane(lane_), mine(lane_ < m_.T), lsem(lds), lcnt(lds + 64 * PPL) {
+  __device__ WEnv(const SflMap& m_, const SflState& s_, uint32_t e_, int lane_, uint32_t* lds, const double* leps_)
+      : m(m_), s(s_), e(e_), E(s_.E), lane(lane_), mine(lane_ < m_.T), lsem(lds), lcnt(lds + 64 * PPL), lpf((double*)(lds + 64 * (PPL + SPL))), leps(leps_) {
     qb = s.q + (size_t)e * m.q_per_env;
+    pf_ok = false;
+    pf_roff = pf_qoff = PF_NONE;
     touchb = s.touched + (size_t)e * m.touched_words;
     slotb = s.slot + (size_t)e * (uint32_t)(m.S * m.T);
   }
@@ -188,12 +207,12 @@ struct WEnv {
   __device__ __forceinline__ size_t ix(size_t i) const { return i * (size_t)E + e; }
 
   // ---- cross-lane access (index wave-uniform) -------------------------------------
-  __device__ __forceinline__ uint32_t sget(int p) const { return lsem[p]; }
+  __device__ __forceinline__ uint32_t sget(int p) const { return uni(lsem[p]); }
   __device__ __forceinline__ void sset(int p, uint32_t r) {
     if (lane == 0) lsem[p] = r;
   }
   __device__ __forceinline__ uint32_t& sem(int k) const { return lsem[k * 64 + lane]; }  // lane-parallel
-  __device__ __forceinline__ uint32_t cget(int sw) const { return lcnt[sw]; }
+  __device__ __forceinline__ uint32_t cget(int sw) const { return uni(lcnt[sw]); }
   __device__ __forceinline__ void cset(int sw, uint32_t v) {
     if (lane == 0) lcnt[sw] = v;
   }
@@ -242,6 +261,29 @@ struct WEnv {
       return 0;
     }
     const int32_t d = ldc(m.dist, ((uint32_t)k * (uint32_t)m.HW + (uint32_t)cell) * 4u + (uint32_t)dir);
+    if (d >= DIST_INF) lerr |= E_INF_DIST;
+    return d;
+  }
+
+  // per-lane projection step of reward_func.py:41-56 (STOP entries are skipped, and a cell off
+  // the grid ends the walk) and distance lookup with the off-grid marker
+  __device__ __forceinline__ void project(uint32_t a, int& pc, int& pd) const {
+    if (a != A_STOP && pc >= 0) {
+      const Move mv = check_action<false>(a, pc, pd);
+      pc = mv.cell;
+      pd = mv.dir;
+    }
+  }
+  __device__ __forceinline__ int32_t dist_v(int k, int cell, int dir) const {
+    if (cell < 0) return PF_OFFGRID;
+    return ld(m.dist, ((uint32_t)k * (uint32_t)m.HW + (uint32_t)cell) * 4u + (uint32_t)dir);
+  }
+  // distance staged by prefetch (dist() semantics: off the grid or unreachable sets E_INF_DIST)
+  __device__ __forceinline__ int32_t dist_staged(int32_t d) {
+    if (d == PF_OFFGRID) {
+      lerr |= E_INF_DIST;
+      return 0;
+    }
     if (d >= DIST_INF) lerr |= E_INF_DIST;
     return d;
   }
@@ -317,9 +359,11 @@ struct WEnv {
   __device__ __forceinline__ double* qbase() const { return qb; }
   __device__ __forceinline__ void touch_row(uint32_t row) const { atomicOr(&touchb[row >> 5], 1u << (row & 31u)); }
   __device__ __forceinline__ double lr_of(uint32_t n) const {
+    if (m.lr_decay == 1.0) return m.lr0;  // lr0 * 1.0**n (distr_q.py:70-79)
     return n < (uint32_t)m.ntab ? ldc(m.lr_tab, (size_t)n) : m.lr0 * pow_ool(m.lr_decay, (double)n);
   }
   __device__ __forceinline__ double lr_of_var(uint32_t n) const {
+    if (m.lr_decay == 1.0) return m.lr0;
     return n < (uint32_t)m.ntab ? ld(m.lr_tab, (size_t)n) : m.lr0 * pow_ool(m.lr_decay, (double)n);
   }
 
@@ -467,6 +511,7 @@ struct WEnv {
   // ---- one Flatland tick + switchfl bookkeeping (switch_env.py:296-401, 427-485;
   //      flatland_lite.RailEnv.step), train-parallel: lane h = train h ----------------------------
   __device__ __forceinline__ void tick() {
+    pf_ok = false;
     const int32_t t = ++now;
     const uint64_t seed = s.seed[e];
     const int h = lane;
@@ -682,6 +727,86 @@ struct WEnv {
     if ((ALL & full) == full || over) flags |= F_TERM;
   }
 
+  // ---- batch prefetch ----------------------------------------------------------------------
+  // When a tick leaves decisions queued, each queued train's lane loads, in parallel, its
+  // (switch, train) slot word, the Q cell of the pending update that slot holds, and the Q row of
+  // its observation as the semaphores stand now, into LDS.  The batch's decisions then run in
+  // handle order as before; a decision uses a staged row only if the row it actually observes
+  // (after the batch's earlier decisions changed the semaphores) is the staged one, and staged
+  // Q values are dropped when the batch writes their cell (pf_written).  Slot words are never
+  // stale: a decision writes only its own train's slots and a train decides once per batch.
+  __device__ __forceinline__ void prefetch(bool greedy) {
+    const uint64_t malf = __ballot(mine && tb_state(bits) == S_MALF);
+    pf_roff = pf_qoff = PF_NONE;
+    if (!((q_mask >> lane) & 1ull)) return;
+    const int sw = (int)(sdec >> 16);
+    double* pfl = lpf + PF_W * lane;
+    const uint64_t slw = ld(slotb, slot_ix(sw, lane));
+    const u4 w0 = ld((const u4*)m.sw_pack, (size_t)sw * 4u);
+    const vec_t<uint32_t, 2> nbw = ld((const vec_t<uint32_t, 2>*)m.sw_pack, (size_t)sw * 8u + 4u);
+    const int32_t la = ld(m.tr_pack, (size_t)lane * 8 + 1), k = ld(m.tr_pack, (size_t)lane * 8 + 2);
+    const int np = (int)(w0[0] & 15u);
+    const int pin = (int)(nprv & 0xFFFFu);
+    int slot = pin & 3;
+    if ((pin >> 2) != sw || slot >= np) slot = 0;
+    uint32_t fb = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int p = 4 * sw + j;
+      const int nb = j < np ? (int)((nbw[j >> 1] >> (16 * (j & 1))) & 0xFFFFu) : p;
+      const uint32_t blk = rec_blocks(lsem[nb], (uint32_t)lane, malf, 0u) | rec_blocks(lsem[p], (uint32_t)lane, malf, 1u);
+      fb |= (blk == 0u && j < np) ? (1u << j) : 0u;
+    }
+    // distances the decision needs (reward_func.py:23-78): at the cell, and at the projection of
+    // the plan the decision leaves (STOP: [STOP] + plan; a route: [front or FWD, final action])
+    int32_t* pfi = (int32_t*)pfl + PF_I;
+    const int dir0 = (int)tb_dir(bits);
+    const int32_t dd = dist_v(k, pos, dir0);
+    pfi[0] = dd;
+    {
+      int pc = pos, pd = dir0;
+      const uint32_t n = pl_len(plan);
+      for (uint32_t i = 0; i < n; ++i) project(pl_at(plan, i), pc, pd);
+      pfi[1] = dist_v(k, pc, pd);
+    }
+    {
+      int pc = pos, pd = dir0;
+      project(pl_len(plan) ? pl_front(plan) : A_FWD, pc, pd);
+#pragma unroll
+      for (uint32_t t = 0; t < 4; ++t) {
+        int qc = pc, qd = pd;
+        project(t, qc, qd);
+        pfi[2 + t] = dist_v(k, qc, qd);
+      }
+    }
+    if (pos >= 0 && dd < DIST_INF) {
+      const int32_t dl = now - la + dd;
+      const int32_t avail = la - t_ed;
+      const uint32_t lvl = dl <= 0 ? 0u : (dl <= avail * 20 ? 1u : 2u);
+      const uint32_t state = ((fb * (uint32_t)m.K) + (uint32_t)k) * 3u + lvl;
+      const u4 pr = ld((const u4*)m.port_pack, (size_t)(4 * sw + slot));
+      const uint32_t w = pr[1] >> 16, roff = pr[3] + state * w;
+      const double* rp = qbase() + roff;
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        if ((uint32_t)c < w) pfl[c] = ld(rp, (size_t)c);
+      pf_roff = roff;
+    }
+    const uint32_t pend = greedy ? PEND_NONE : slot_pend(slw, epoch);
+    if (pend != PEND_NONE) {
+      const u4 pr = ld((const u4*)m.port_pack, (size_t)(4 * (pend & 0xFFFu) + ((pend >> 12) & 3u)));
+      const uint32_t qoff = pr[3] + ((pend >> 14) & 0x3FFFu) * (pr[1] >> 16) + ((pend >> 28) & 3u);
+      pfl[4] = ld(qbase(), (size_t)qoff);
+      pf_qoff = qoff;
+    }
+    pfl[5] = __longlong_as_double((long long)slw);
+  }
+  // a Q cell of this env was written (uniform offset): drop staged copies that contain it
+  __device__ __forceinline__ void pf_written(uint32_t off) {
+    pf_qoff = (pf_qoff == off) ? PF_NONE : pf_qoff;
+    pf_roff = (off - pf_roff < 4u) ? PF_NONE : pf_roff;
+  }
+
   // ---- decision (wave-uniform): observe (observer.py:246-308), epsilon-greedy
   //      (distr_q.py:312-319), _apply_action (switch_env.py:203-294) ---------------------------
   struct Dec {
@@ -692,7 +817,7 @@ struct WEnv {
     int next_sw;
     uint64_t slotword;
     double mq;        // max over the full decision row (successor value for the pending update)
-    double* qp_pend;  // Q cell of the pending update consumed by this decision (or null)
+    uint32_t qoff_pend;  // Q cell (offset in the env's block) of the pending update consumed here, or PF_NONE
     double q_pend;    // its value, loaded during the decision
     uint32_t row_pend;  // key-set row of the pending update
   };
@@ -700,13 +825,21 @@ struct WEnv {
   __device__ __forceinline__ void decide(Dec& d, bool greedy) {
     SFL_PT(t_obs);
     // agent_iter: lowest queued train (switch_env.py:418-421, 616-622)
+    if (!pf_ok) {
+      prefetch(greedy);
+      pf_ok = true;
+      SFL_PCNT(3);
+    }
+    SFL_PCNT(8);
     const int h = ctz64(q_mask);
     q_mask &= q_mask - 1ull;
     const uint32_t sd = rl(sdec, h);
     const int sw = (int)(sd >> 16);
     const SwRec swr = sw_rec(sw);
     const vec_t<int32_t, 8> tr = ldcv<vec_t<int32_t, 8>>(m.tr_pack, (size_t)h);
-    const uint64_t slot_v = ld(slotb, slot_ix(sw, h));  // made uniform when needed
+    const double* pfh = lpf + PF_W * h;
+    const uint64_t slot_v = (uint64_t)__double_as_longlong(pfh[5]);  // staged by prefetch (never stale)
+    const uint32_t pf_roff_h = rl(pf_roff, h), pf_qoff_h = rl(pf_qoff, h);
     const int np = swr.np();
     const int na = swr.na();
     const uint32_t npv = rl(nprv, h);
@@ -732,7 +865,8 @@ struct WEnv {
     const uint32_t b = rl(bits, h);
     const int32_t p0 = rl(pos, h);
     const int32_t ed = tr[0], la = tr[1], k = tr[2];
-    const int32_t dl = now - la + dist(k, p0, (int)tb_dir(b));
+    const int32_t* pfih = (const int32_t*)pfh + PF_I;
+    const int32_t dl = now - la + dist_staged(uni(pfih[0]));
     const int32_t avail = la - ed;
     const uint32_t lvl = dl <= 0 ? 0u : (dl <= avail * 20 ? 1u : 2u);
     const uint32_t state = ((free_bits * (uint32_t)m.K) + (uint32_t)k) * 3u + lvl;
@@ -746,13 +880,20 @@ struct WEnv {
     // issue the Q row load and the pending update's Q cell load, then draw while they fly
     const PortRec prr = port_rec(4 * sw + slot);
     const int w = prr.q_w();
-    const double* rp = qbase() + (prr.q_off() + state * (uint32_t)w);
-    // lane c < w holds compact column c of the row
+    const uint32_t roff = prr.q_off() + state * (uint32_t)w;
+    // lane c < w holds compact column c of the row (staged by prefetch unless stale)
     const bool colv = lane < w;
-    const double v_c = ld(rp, (size_t)(colv ? lane : 0));
+    double v_c;
+    if (pf_roff_h == roff) {
+      v_c = pfh[lane & 3];
+      SFL_PCNT(4);
+    } else {
+      v_c = ld(qbase() + roff, (size_t)(colv ? lane : 0));
+      SFL_PCNT(5);
+    }
     d.slotword = uni(slot_v);
     const uint32_t pend = greedy ? PEND_NONE : slot_pend(d.slotword, epoch);
-    d.qp_pend = nullptr;
+    d.qoff_pend = PF_NONE;
     double q_pend_v = 0.0;
     if (pend != PEND_NONE) {
       const int ps = (int)(pend & 0xFFFu);
@@ -760,9 +901,15 @@ struct WEnv {
       const uint32_t pstate = (pend >> 14) & 0x3FFFu;
       const int pj = (int)((pend >> 28) & 3u);
       const PortRec pr = port_rec(4 * ps + pslot);
-      d.qp_pend = qbase() + pr.q_off() + (size_t)pstate * (uint32_t)pr.q_w() + pj;
+      d.qoff_pend = pr.q_off() + pstate * (uint32_t)pr.q_w() + (uint32_t)pj;
       d.row_pend = pr.row_base() + pstate;
-      q_pend_v = ld(d.qp_pend, 0);
+      if (pf_qoff_h == d.qoff_pend) {
+        q_pend_v = pfh[4];
+        SFL_PCNT(6);
+      } else {
+        q_pend_v = ld(qbase(), (size_t)d.qoff_pend);
+        SFL_PCNT(7);
+      }
     }
     const int32_t reward = slot_rew(d.slotword, epoch);
     // epsilon-greedy
@@ -770,8 +917,10 @@ struct WEnv {
     bool explore = false;
     if (!greedy) {
       const uint32_t n = cget(sw);
-      const double eps = n < (uint32_t)m.ntab ? ldc(m.eps_tab, (size_t)n) : m.eps0 * pow_ool(m.eps_decay, (double)n);
-      if (pcg_double(rng) < eps) {
+      const double eps = n < (uint32_t)EPS_WIN && n < (uint32_t)m.ntab ? unid(leps[n])
+                         : n < (uint32_t)m.ntab                      ? ldc(m.eps_tab, (size_t)n)
+                                                                     : m.eps0 * pow_ool(m.eps_decay, (double)n);
+      if (unid(pcg_double(rng)) < eps) {
         explore = true;
         const uint32_t sub_seed = pcg_bounded(rng, 2147483646u);
         Pcg64 sub;
@@ -882,18 +1031,9 @@ struct WEnv {
         if ((free_bits >> swr.dst(a)) & 1u) all_blocked = false;
       }
     }
-    // reward_func.py:23-78: project the position along the non-STOP plan
-    int pc = p0, pd = (int)tb_dir(b);
-    const uint32_t nn = pl_len(p);
-    for (uint32_t i = 0; i < nn; ++i) {
-      const uint32_t a = pl_at(p, i);
-      if (a == A_STOP) continue;
-      if (pc < 0) break;
-      Move mv = check_action<true>(a, pc, pd);
-      pc = mv.cell;
-      pd = mv.dir;
-    }
-    const int32_t cur = now - la + dist(k, pc, pd);
+    // reward_func.py:23-78: distance at the position projected along the non-STOP plan (staged
+    // by prefetch for the STOP plan and for each final rail action of a route)
+    const int32_t cur = now - la + dist_staged(uni(moving ? pfih[2 + (turn & 3u)] : pfih[1]));
     const int32_t diff = rl(delay, h) - cur;
     d.r_new = (pl_front(p) == A_STOP && !all_blocked) ? diff - 1300 : diff;
     tset(delay, h, cur);
@@ -917,7 +1057,7 @@ struct WEnv {
       if (lane == 0) st(slotb, slot_ix(d.next_sw, d.h), slot_make(PEND_NONE, d.r_new, epoch));
       return;
     }
-    if (d.qp_pend) {
+    if (d.qoff_pend != PF_NONE) {
       const uint32_t pend = slot_pend(d.slotword, epoch);
       const int ps = (int)(pend & 0xFFFu);
       const double lr = lr_of(cget(ps));
@@ -933,10 +1073,11 @@ struct WEnv {
         nv = a1 + b1;
       }
       if (lane == 0) {
-        st(d.qp_pend, 0, nv);
+        st(qbase(), (size_t)d.qoff_pend, nv);
         touch_row(d.row_pend);
         if (d.sw != ps) touch_row(port_rec(4 * d.sw + d.slot).row_base() + d.state);
       }
+      pf_written(d.qoff_pend);
     }
     if (lane == 0) {
       st(slotb, slot_ix(d.sw, d.h), slot_make(PEND_NONE, slot_rew(d.slotword, epoch), epoch));
@@ -948,6 +1089,7 @@ struct WEnv {
     // same successor switch => same slot), so the lanes' updates are independent.
     uint64_t fresh = arr_mask & ~fl_mask;
     fl_mask |= fresh;
+    if (fresh) pf_ok = false;  // bonus writes: stage the rest of the batch again
     while (fresh) {
       const int tr = ctz64(fresh);
       fresh &= fresh - 1ull;
@@ -992,11 +1134,15 @@ struct WEnv {
 template <int PPL, int SPL>
 __device__ void run(const SflMap& m, const SflState& s, const SflCtl& c) {
   using V = WEnv<PPL, SPL>;
+  constexpr int LDS_WORDS = 64 * (PPL + SPL) + 64 * PF_W * 2;  // semaphores, counters, prefetch
   const int lane = (int)__lane_id();
   const uint32_t e = uni((uint32_t)((blockIdx.x * blockDim.x + threadIdx.x) >> 6));
+  __shared__ double leps[EPS_WIN];
+  for (int i = (int)threadIdx.x; i < EPS_WIN; i += (int)blockDim.x) leps[i] = i < m.ntab ? m.eps_tab[i] : 0.0;
+  __syncthreads();
   if (e >= s.E) return;
-  __shared__ uint32_t lds[4 * 64 * (PPL + SPL)];
-  V v(m, s, e, lane, lds + (threadIdx.x >> 6) * 64 * (PPL + SPL));
+  __shared__ uint32_t lds[4 * LDS_WORDS];
+  V v(m, s, e, lane, lds + (threadIdx.x >> 6) * LDS_WORDS, leps);
   v.load();
   int32_t phase = uni(ld(s.phase, e));
   int32_t ep_t = uni(ld(s.ep_t, e)), n_test = uni(ld(s.n_test, e));
@@ -1006,7 +1152,7 @@ __device__ void run(const SflMap& m, const SflState& s, const SflCtl& c) {
   d.state = 0;
   d.slotword = 0;
   d.mq = d.q_pend = 0.0;
-  d.qp_pend = nullptr;
+  d.qoff_pend = PF_NONE;
   d.row_pend = 0;
   const bool test_mode = c.mode == 1;
 #ifdef SFL_PROFILE
@@ -1113,7 +1259,7 @@ __device__ void run(const SflMap& m, const SflState& s, const SflCtl& c) {
   prof[4] = (uint64_t)__builtin_amdgcn_s_memtime() - t_begin;
   if (lane == 0) {
     for (int k = 0; k < 5; ++k) atomicAdd(&g_prof[k], (unsigned long long)prof[k]);
-    for (int k = 0; k < 3; ++k) atomicAdd(&g_prof[5 + k], (unsigned long long)v.prof[k]);
+    for (int k = 0; k < 9; ++k) atomicAdd(&g_prof[5 + k], (unsigned long long)v.prof[k]);
   }
 #endif
   if (lane == 0) {
