@@ -69,7 +69,12 @@ def main():
     ap.add_argument("--config", default="c3")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--partition", action="store_true",
+                    help="graph-partitioned mode (BASELINE configs[4]): switch agents owned by ranks, RCCL all-to-all "
+                         "of row lookups and updates; defaults to --config c5 --envs 8192")
     args = ap.parse_args()
+    if args.partition:
+        return bench_partition(args)
 
     import torch
     par = importlib.import_module(PKG + ".parallel")
@@ -148,6 +153,70 @@ def main():
             res["cpu_baseline"] = cpu_baseline(sc, args.cpu_seconds)
         print(json.dumps(res), flush=True)
     b.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def bench_partition(args):
+    """configs[4]: the 256-switch map with its switch agents graph-partitioned over the ranks; each rank
+    simulates its own envs and owns the Q rows of its switches for every env (weak scaling: envs and owned
+    Q bytes per GPU fixed).  A step = every env makes --decisions decisions = decisions + 1 message rounds."""
+    import torch
+    par = importlib.import_module(PKG + ".parallel")
+    part = importlib.import_module(PKG + ".partition")
+    world, rank, local = par.world()
+    dist = par.init("nccl")
+    torch.cuda.set_device(local)
+    mapgen = importlib.import_module(PKG + ".mapgen")
+    comp = importlib.import_module(PKG + ".compiler")
+    cfg = args.config if args.config != "c3" else "c5"
+    E = args.envs if args.envs != 65536 else 8192
+    cm = comp.compile_scenario(mapgen.make_config(cfg))
+    seeds = par.shard_seeds(450565, E, rank)
+    pb = part.PartitionedBatch(cm, HP, seeds, rank * E, world * E, rank=rank, world=world, dist=dist, device=local,
+                               buffer_device="cuda")
+    pb.learn_begin()
+    pb.apply_qinit()
+    for _ in range(args.warmup):
+        pb.step(args.decisions)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    barrier()
+    t0 = time.perf_counter()
+    rounds = 0
+    for _ in range(args.steps):
+        rounds += pb.step(args.decisions)
+    barrier()
+    dt = time.perf_counter() - t0
+    total = float(E * args.decisions * args.steps)
+    dt, total_all = par.reduce_timing(dist, dt, total, device="cuda")
+    if rank == 0:
+        res = {
+            "metric": METRIC,
+            "value": total_all / dt,
+            "unit": "agent-env-steps/sec",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": dt * 1e3 / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": f"synthetic {cm.S}-switch/{cm.T}-train Flatland-format map (mapgen {cfg}, seed 450565)",
+            "config": {"workload": f"{cfg}: {cm.S} switches / {cm.T} trains, switch agents graph-partitioned over "
+                                   f"{world} rank(s) (BFS blocks, cut {part.cut_fraction(cm, pb.owner):.2f}), {E} envs "
+                                   f"per GPU, {args.decisions} agent-env-steps per env per step",
+                       "envs_per_gpu": E, "decisions_per_env_per_step": args.decisions,
+                       "rounds_per_step": rounds / max(1, args.steps),
+                       "parallelism": f"env-batch dp{world} x switch-agent partition {world}"},
+        }
+        print(json.dumps(res), flush=True)
+    pb.close()
     if dist is not None:
         dist.destroy_process_group()
 

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define SFL_ABI_VERSION 2
+#define SFL_ABI_VERSION 3
 
 typedef struct sfl_handle sfl_handle;
 
@@ -140,6 +140,29 @@ int sfl_get_counters(sfl_handle* h, sfl_counters* out);
 /* read back one env's state word arrays (debug / parity tests) */
 int sfl_get_env_state(sfl_handle* h, uint32_t env, int32_t* elapsed, int32_t* phase, uint64_t* sem /* [4S] */,
                       int32_t* tr_pos /* [T] */, uint32_t* tr_bits /* [T] */);
+
+/* ---- graph-partitioned mode (BASELINE.json configs[4]; SURVEY.md §8(e) "C5") ----
+ * The switch agents are partitioned over `world` ranks (owner[S]); rank r stores the Q rows of
+ * the switches it owns for all `envs_total` envs of the job, and simulates its own envs
+ * [env_base, env_base + n_envs).  A round: sfl_part_local (every local env applies the reply
+ * to its last request, runs to its next decision and writes that decision's request, plus the
+ * update records of its post step), an all-to-all of the update and request buffers,
+ * sfl_part_update + sfl_part_answer on the received records, and an all-to-all of the replies
+ * back.  Buffers are [world][cap + 1] records (record 0 of a segment = header holding the
+ * count); on the GPU they are device pointers (the caller's RCCL buffers).  Replaces the
+ * reference's in-process successor lookup max_q(next_state, next_agent) and update
+ * (switchfl/distr_q.py:419-466) across GPU boundaries. */
+int sfl_part_config(sfl_handle* h, int32_t rank, int32_t world, const int32_t* owner /* [S] */, uint32_t env_base,
+                    uint32_t envs_total, uint32_t cap_req /* >= n_envs */, uint32_t cap_upd);
+int sfl_part_record_sizes(uint32_t* req, uint32_t* rep, uint32_t* upd);
+int sfl_part_begin(sfl_handle* h);  /* start a part step: per-env decision counters to 0 */
+int sfl_part_local(sfl_handle* h, int64_t decisions_per_env, const void* replies, void* requests, void* updates,
+                   uint64_t* requests_sent);
+int sfl_part_update(sfl_handle* h, const void* updates);
+int sfl_part_answer(sfl_handle* h, const void* requests, void* replies);
+/* owned Q blocks of one env of the job, written into the full per-env layout of sfl_get_q
+ * (other entries untouched); owned key-set bits OR-ed into touched */
+int sfl_part_get_q(sfl_handle* h, uint32_t global_env, double* q, uint32_t* touched);
 
 #ifdef __cplusplus
 }

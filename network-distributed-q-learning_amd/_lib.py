@@ -12,6 +12,7 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 PRODUCT_LIB = os.path.join(HERE, "libsfl.so")
+ABI_VERSION = 3  # include/sfl.h SFL_ABI_VERSION
 
 P = C.POINTER
 
@@ -74,6 +75,15 @@ EXPORTS = {
     "sfl_get_counters": (C.c_int, [C.c_void_p, P(Counters)]),
     "sfl_get_env_state": (C.c_int, [C.c_void_p, C.c_uint32, P(C.c_int32), P(C.c_int32), P(C.c_uint64),
                                     P(C.c_int32), P(C.c_uint32)]),
+    # graph-partitioned mode (partition.py)
+    "sfl_part_config": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, P(C.c_int32), C.c_uint32, C.c_uint32,
+                                  C.c_uint32, C.c_uint32]),
+    "sfl_part_record_sizes": (C.c_int, [P(C.c_uint32), P(C.c_uint32), P(C.c_uint32)]),
+    "sfl_part_begin": (C.c_int, [C.c_void_p]),
+    "sfl_part_local": (C.c_int, [C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p, P(C.c_uint64)]),
+    "sfl_part_update": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "sfl_part_answer": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
+    "sfl_part_get_q": (C.c_int, [C.c_void_p, C.c_uint32, P(C.c_double), P(C.c_uint32)]),
 }
 
 
@@ -91,7 +101,7 @@ class Lib:
             fn = getattr(self.dll, name)
             fn.restype = res
             fn.argtypes = args
-        if self.dll.sfl_abi_version() != 2:
+        if self.dll.sfl_abi_version() != ABI_VERSION:
             raise SflError("ABI version mismatch")
 
     def check(self, rc: int, what: str):
@@ -111,6 +121,10 @@ def load_product() -> Lib:
     """The HIP library; raises if it is missing or no GPU is visible (no fallback)."""
     global _product
     if _product is None:
+        # one HIP runtime per process: load torch's (it carries its own libamdhip64.so.7 / HSA runtime)
+        # before libsfl.so resolves the same soname, so the library and torch's RCCL / allocator share it
+        import torch  # noqa: F401
+
         # SFL_LIB: an alternative in-tree build of the same HIP sources (tuning sweeps)
         lib = Lib(os.environ.get("SFL_LIB", PRODUCT_LIB))
         if lib.device_count() < 1:

@@ -40,6 +40,40 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SFL_WA
   sfl::wave::run<PPL, SPL>(*m, *s, *c);
 }
 
+// graph-partitioned rounds (sfl_part.h): local env step (lane per env), segment headers,
+// owner-side answer and update (one thread per record)
+template <int NW>
+__global__ void __launch_bounds__(256) k_part_local(const sfl::SflMap* __restrict__ m, const sfl::SflState* __restrict__ s,
+                                                    const sfl::SflCtl* __restrict__ c, const sfl::SflPart* __restrict__ P) {
+  const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < s->E) sfl::env_run_part<NW>(*m, *s, *c, *P, e);
+}
+__global__ void k_part_headers(const sfl::SflPart* __restrict__ P) {
+  if ((int)threadIdx.x < P->world) sfl::part_headers(*P, (int)threadIdx.x);
+}
+__global__ void k_part_answer(const sfl::SflMap* __restrict__ m, const sfl::SflPart* __restrict__ P,
+                              const sfl::PartReq* __restrict__ in, sfl::PartRep* __restrict__ out) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t cap = P->cap_req;
+  const size_t g = i / cap, k = i % cap + 1;
+  if (g >= (size_t)P->world) return;
+  const size_t base = g * (cap + 1);
+  if (k <= in[base].genv) sfl::part_answer_one(*m, *P, in[base + k], out[base + k]);
+}
+__global__ void k_part_update(const sfl::SflMap* __restrict__ m, const sfl::SflPart* __restrict__ P,
+                              const sfl::PartUpd* __restrict__ in, int stage) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t cap = P->cap_upd;
+  const size_t g = i / cap, k = i % cap + 1;
+  if (g >= (size_t)P->world) return;
+  const size_t base = g * (cap + 1);
+  if (k <= in[base].genv && in[base + k].stage == stage) sfl::part_update_one(*m, *P, in[base + k]);
+}
+__global__ void k_replicate(uint32_t* base, size_t words, uint32_t n) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < words * (n - 1); i += (size_t)gridDim.x * blockDim.x)
+    base[words + i] = base[i % words];
+}
+
 __global__ void k_fill_f64(double* p, double v, size_t n) {
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) p[i] = v;
 }
@@ -98,6 +132,7 @@ struct HipBackend {
     if (ev0) hipEventDestroy(ev0);
     if (ev1) hipEventDestroy(ev1);
     if (d_params) hipFree(d_params);
+    if (d_pparams) hipFree(d_pparams);
     if (stream) hipStreamDestroy(stream);
   }
   void* alloc(size_t bytes) {
@@ -176,6 +211,68 @@ struct HipBackend {
     return err.empty() ? 0 : -1;
   }
   int sync() { return check(hipStreamSynchronize(stream), "sync") && err.empty() ? 0 : -1; }
+  void replicate(void* base, size_t bytes, uint32_t n) {
+    if (n > 1) k_replicate<<<4096, 256, 0, stream>>>((uint32_t*)base, bytes / 4, n);
+    check(hipGetLastError(), "k_replicate");
+  }
+  // parameter block for the partitioned kernels: SflMap | SflState | SflCtl | SflPart
+  struct PartParams {
+    sfl::SflMap m;
+    char p0[(sizeof(sfl::SflMap) + 63) / 64 * 64 - sizeof(sfl::SflMap)];
+    sfl::SflState s;
+    char p1[(sizeof(sfl::SflState) + 63) / 64 * 64 - sizeof(sfl::SflState)];
+    sfl::SflCtl c;
+    char p2[(sizeof(sfl::SflCtl) + 63) / 64 * 64 - sizeof(sfl::SflCtl)];
+    sfl::SflPart P;
+  };
+  void* d_pparams = nullptr;
+  PartParams* part_params(const sfl::SflMap& m, const sfl::SflState& s, const sfl::SflCtl& c, const sfl::SflPart& P) {
+    static_assert(sizeof(PartParams) <= 4096, "params");
+    if (!d_pparams && !check(hipMalloc(&d_pparams, 4096), "hipMalloc params")) return nullptr;
+    PartParams hp;
+    hp.m = m;
+    hp.s = s;
+    hp.c = c;
+    hp.P = P;
+    check(hipMemcpyAsync(d_pparams, &hp, sizeof hp, hipMemcpyHostToDevice, stream), "params h2d");
+    // the copy source is on the stack: complete it before returning
+    check(hipStreamSynchronize(stream), "params sync");
+    return (PartParams*)d_pparams;
+  }
+  int part_local(const sfl::SflMap& m, const sfl::SflState& s, const sfl::SflCtl& c, const sfl::SflPart& P, float* ms) {
+    PartParams* pp = part_params(m, s, c, P);
+    if (!pp) return -1;
+    check(hipEventRecord(ev0, stream), "event");
+    // one wave per block: a round's envs spread over as many CUs as possible
+    const unsigned blocks = (s.E + 63) / 64;
+    if (m.T <= 32) k_part_local<1><<<blocks, 64, 0, stream>>>(&pp->m, &pp->s, &pp->c, &pp->P);
+    else if (m.T <= 64) k_part_local<2><<<blocks, 64, 0, stream>>>(&pp->m, &pp->s, &pp->c, &pp->P);
+    else k_part_local<4><<<blocks, 64, 0, stream>>>(&pp->m, &pp->s, &pp->c, &pp->P);
+    if (!check(hipGetLastError(), "k_part_local")) return -1;
+    k_part_headers<<<1, 256, 0, stream>>>(&pp->P);
+    check(hipEventRecord(ev1, stream), "event");
+    if (!check(hipEventSynchronize(ev1), "k_part_local")) return -1;
+    hipEventElapsedTime(ms, ev0, ev1);
+    return err.empty() ? 0 : -1;
+  }
+  void part_answer(const sfl::SflMap& m, const sfl::SflPart& P, const sfl::PartReq* in, sfl::PartRep* out) {
+    sfl::SflState s{};
+    sfl::SflCtl c{};
+    PartParams* pp = part_params(m, s, c, P);
+    if (!pp) return;
+    const size_t n = (size_t)P.world * P.cap_req;
+    k_part_answer<<<(unsigned)((n + 255) / 256), 256, 0, stream>>>(&pp->m, &pp->P, in, out);
+    check(hipGetLastError(), "k_part_answer");
+  }
+  void part_update(const sfl::SflMap& m, const sfl::SflPart& P, const sfl::PartUpd* in, int stage) {
+    sfl::SflState s{};
+    sfl::SflCtl c{};
+    PartParams* pp = part_params(m, s, c, P);
+    if (!pp) return;
+    const size_t n = (size_t)P.world * P.cap_upd;
+    k_part_update<<<(unsigned)((n + 255) / 256), 256, 0, stream>>>(&pp->m, &pp->P, in, stage);
+    check(hipGetLastError(), "k_part_update");
+  }
 };
 
 }  // namespace

@@ -870,8 +870,16 @@ SFL_FN int transition_train(V& v, int h, int in_p, int out_p) {
   return target >> 2;
 }
 
+// The decision of one agent_iter step, up to the point where the Q row is needed: the
+// observation (observer.py:246-308) and the epsilon draw (distr_q.py:312-319).
+struct Obs {
+  int32_t h, sw, slot, explore, action;
+  uint32_t state, amask;
+  int32_t reward;
+};
+
 template <class V>
-SFL_FN void env_decide(V& v, Decision& d, bool greedy) {
+SFL_FN void decide_observe(V& v, Obs& o, bool greedy) {
   const SflMap& m = v.m;
   const SflState& s = v.s;
   // agent_iter: lowest queued train (switch_env.py:418-421, 616-622)
@@ -909,17 +917,20 @@ SFL_FN void env_decide(V& v, Decision& d, bool greedy) {
   uint32_t amask = 1u << (na - 1);
   for (int a = 0; a < na - 1; ++a)
     if (m.act_src[sw * 8 + a] == (uint8_t)slot && ((free_bits >> m.act_dst[sw * 8 + a]) & 1u)) amask |= 1u << a;
-  const int32_t reward = slot_rew(s.slot[v.ix((size_t)sw * m.T + h)], v.epoch);
-
-  // epsilon-greedy
-  int action;
-  const double* row = v.qrow(sw, slot, state);
-  bool explore = false;
+  o.h = h;
+  o.sw = sw;
+  o.slot = slot;
+  o.state = state;
+  o.amask = amask;
+  o.reward = slot_rew(s.slot[v.ix((size_t)sw * m.T + h)], v.epoch);
+  o.explore = 0;
+  o.action = -1;
+  // epsilon-greedy: the exploratory branch needs no Q value
   if (!greedy) {
     Pcg64 g = v.rng_load();
     const double eps = v.eps_of(s.counts[v.ix(sw)]);
     if (pcg_double(g) < eps) {
-      explore = true;
+      o.explore = 1;
       const uint32_t sub_seed = pcg_bounded(g, 2147483646u);
       Pcg64 sub;
       pcg_from_seedseq(sub_seed, sub);
@@ -927,17 +938,23 @@ SFL_FN void env_decide(V& v, Decision& d, bool greedy) {
       uint32_t pick = pcg_bounded(sub, nvalid - 1u);
       uint32_t mk = amask;
       for (uint32_t k = 0; k < pick; ++k) mk &= mk - 1u;
-      action = ctz32(mk);
+      o.action = ctz32(mk);
     }
     v.rng_store(g);
   }
-  if (!explore) {
-    v.touch(sw, slot, state);
-    action = max_action(v, sw, slot, row, amask);
-  }
-  if (action < 0 || action >= na) v.err |= E_BAD_ACTION;
+}
 
-  // _apply_action
+// _apply_action (switch_env.py:203-294) for the chosen action
+template <class V>
+SFL_FN void decide_apply(V& v, const Obs& o, int action, Decision& d) {
+  const SflMap& m = v.m;
+  const SflState& s = v.s;
+  const int h = o.h, sw = o.sw, slot = o.slot;
+  const int na = m.sw_na[sw];
+  const int pin = v.next_port(h);
+  const uint32_t b = v.bits(h);
+  const int32_t pos = v.pos(h);
+  if (action < 0 || action >= na) v.err |= E_BAD_ACTION;
   const int stop = na - 1;
   bool moving = false;
   uint32_t turn = A_FWD;
@@ -975,8 +992,8 @@ SFL_FN void env_decide(V& v, Decision& d, bool greedy) {
     all_blocked = true;
     for (int a = 0; a < na - 1; ++a) {
       if (m.act_src[sw * 8 + a] != (uint8_t)slot) continue;
-      const int o = 4 * sw + m.act_dst[sw * 8 + a];
-      if (!v.port_blocked(m.port_nb[o], o, h)) all_blocked = false;
+      const int o2 = 4 * sw + m.act_dst[sw * 8 + a];
+      if (!v.port_blocked(m.port_nb[o2], o2, h)) all_blocked = false;
     }
   }
   // reward_func.py:23-78: project the position along the non-STOP plan
@@ -1000,16 +1017,46 @@ SFL_FN void env_decide(V& v, Decision& d, bool greedy) {
   d.sw = sw;
   d.h = h;
   d.slot = slot;
-  d.state = state;
+  d.state = o.state;
   d.action = action;
   d.j = (action == stop) ? (m.q_w[4 * sw + slot] - 1) : m.act_j[sw * 8 + action];
-  d.reward = reward;
+  d.reward = o.reward;
   d.next_sw = next_sw;
 }
 
-// post-step part of the learn loop (distr_q.py:322-362)
 template <class V>
-SFL_FN void env_post(V& v, const Decision& d) {
+SFL_FN void env_decide(V& v, Decision& d, bool greedy) {
+  Obs o;
+  decide_observe(v, o, greedy);
+  int action = o.action;
+  if (!o.explore) {
+    v.touch(o.sw, o.slot, o.state);
+    action = max_action(v, o.sw, o.slot, v.qrow(o.sw, o.slot, o.state), o.amask);
+  }
+  decide_apply(v, o, action, d);
+}
+
+// Q-table access of the post step.  LocalQ: this env's own table (the fused kernels);
+// the graph-partitioned mode (sfl_part.h) sends the same operations to the switch's owner.
+template <class V>
+struct LocalQ {
+  V& v;
+  SFL_FN void touch(int sw, int slot, uint32_t state) { v.touch(sw, slot, state); }
+  SFL_FN double row_max_of(const Decision& d) { return row_max(v, d.sw, d.slot, v.qrow(d.sw, d.slot, d.state)); }
+  // q <- (1 - lr) * q + lr * target, the reference's operation order (distr_q.py:436-447)
+  SFL_FN void update(int ps, int pslot, uint32_t pstate, int pj, double lr, double target, int /*stage*/) {
+    double* q = v.qrow(ps, pslot, pstate) + pj;
+    const double a = (1.0 - lr) * *q;
+    const double bb = lr * target;
+    *q = a + bb;
+  }
+};
+
+// post-step part of the learn loop (distr_q.py:322-362).  stage: 0 for the pending update,
+// 1 + i for the destination bonus of the i-th newly arrived train (operations of one stage
+// never touch the same Q cell; stages must be applied in order).
+template <class V, class Q>
+SFL_FN void env_post(V& v, const Decision& d, Q& q) {
   const SflMap& m = v.m;
   const SflState& s = v.s;
   uint64_t& here = s.slot[v.ix((size_t)d.sw * m.T + d.h)];
@@ -1019,26 +1066,22 @@ SFL_FN void env_post(V& v, const Decision& d) {
     const int pslot = (int)((pend >> 12) & 3u);
     const uint32_t pstate = (pend >> 14) & 0x3FFFu;
     const int pj = (int)((pend >> 28) & 3u);
-    v.touch(ps, pslot, pstate);
+    q.touch(ps, pslot, pstate);
     const double lr = v.lr_of(s.counts[v.ix(ps)]);
-    double* q = v.qrow(ps, pslot, pstate) + pj;
     const double r = (double)d.reward;
     if (d.sw != ps) {
-      v.touch(d.sw, d.slot, d.state);
-      const double mq = row_max(v, d.sw, d.slot, v.qrow(d.sw, d.slot, d.state));
-      const double a = (1.0 - lr) * *q;
-      const double bb = lr * (r + m.gamma * mq);
-      *q = a + bb;
+      q.touch(d.sw, d.slot, d.state);
+      const double mq = q.row_max_of(d);
+      q.update(ps, pslot, pstate, pj, lr, r + m.gamma * mq, 0);
     } else {
-      const double a = (1.0 - lr) * *q;
-      const double bb = lr * r;
-      *q = a + bb;
+      q.update(ps, pslot, pstate, pj, lr, r, 0);
     }
     here = slot_make(PEND_NONE, slot_rew(here, v.epoch), v.epoch);
   }
   uint64_t& nxt = s.slot[v.ix((size_t)d.next_sw * m.T + d.h)];
   nxt = slot_make(pend_make((uint32_t)d.sw, (uint32_t)d.slot, d.state, (uint32_t)d.j), slot_rew(nxt, v.epoch), v.epoch);
   // destination bonus for newly arrived trains (distr_q.py:344-356)
+  int stage = 1;
 #pragma unroll
   for (int w = 0; w < V::kNW; ++w) {
     uint32_t fresh = v.msk[1][w] & ~v.msk[2][w];
@@ -1055,17 +1098,21 @@ SFL_FN void env_post(V& v, const Decision& d) {
         const int pslot = (int)((pe >> 12) & 3u);
         const uint32_t pstate = (pe >> 14) & 0x3FFFu;
         const int pj = (int)((pe >> 28) & 3u);
-        v.touch(ps, pslot, pstate);
+        q.touch(ps, pslot, pstate);
         const double lr = v.lr_of(s.counts[v.ix(ps)]);
-        double* q = v.qrow(ps, pslot, pstate) + pj;
-        const double a = (1.0 - lr) * *q;
-        const double bb = lr * (1000.0 + m.gamma * 0.0);
-        *q = a + bb;
+        q.update(ps, pslot, pstate, pj, lr, 1000.0 + m.gamma * 0.0, stage);
         sl = slot_make(PEND_NONE, slot_rew(sl, v.epoch), v.epoch);
       }
+      ++stage;
     }
   }
   s.counts[v.ix(d.sw)] += 1u;
+}
+
+template <class V>
+SFL_FN void env_post(V& v, const Decision& d) {
+  LocalQ<V> q{v};
+  env_post(v, d, q);
 }
 
 // order-independent checksum of the semaphore table (trace/debug only)

@@ -14,6 +14,7 @@
 
 #include "../../include/sfl.h"
 #include "sfl_core.h"
+#include "sfl_part.h"
 
 namespace sfl {
 
@@ -41,6 +42,12 @@ struct Handle {
   float last_kernel_ms = 0.f;
   std::vector<std::vector<uint32_t>> keep;  // host sources of async uploads, alive until the create() sync
   int variant = 0;  // 0: k_run (lane per env); v > 0: k_wave shape kVariants[v] (see choose_variant)
+  // host copies of the map fields the partitioned mode lays out its owned Q blocks with
+  std::vector<uint8_t> h_sw_np, h_q_w;
+  std::vector<uint64_t> h_q_off;
+  std::vector<uint32_t> h_row_base;
+  // graph-partitioned mode (sfl_part.h); part.world == 0: not configured
+  SflPart part{};
 
   template <class T>
   T* dalloc(size_t n) {
@@ -55,6 +62,15 @@ struct Handle {
     T* d = dalloc<T>(n);
     if (d && src && n) be.h2d(d, src, n * sizeof(T));
     return d;
+  }
+  void dfree(void* p) {
+    for (auto& a : allocs)
+      if (a == p) {
+        be.free(p);
+        a = allocs.back();
+        allocs.pop_back();
+        return;
+      }
   }
   ~Handle() {
     for (void* p : allocs) be.free(p);
@@ -108,6 +124,10 @@ int create(const sfl_map_desc* md, const sfl_hparams* hp, uint32_t n_envs, const
     return fail(std::string("sfl_create: backend init failed: ") + h->be.error());
   }
   h->E = n_envs;
+  h->h_sw_np.assign(md->sw_np, md->sw_np + md->S);
+  h->h_q_w.assign(md->q_w, md->q_w + (size_t)md->S * 4);
+  h->h_q_off.assign(md->q_off, md->q_off + (size_t)md->S * 4);
+  h->h_row_base.assign(md->row_base, md->row_base + (size_t)md->S * 4);
   h->variant = choose_variant(md, B::kHasWave);
   SflMap& m = h->map;
   const size_t HW = (size_t)md->H * md->W, NP = (size_t)md->S * 4, S = md->S, T = md->T;
@@ -411,6 +431,7 @@ int check_errors(Handle<B>* h) {
 
 template <class B>
 int run(Handle<B>* h, const SflCtl& c_in, sfl_run_args* args) {
+  if (h->part.world) return fail("sfl_run: the handle is graph-partitioned; drive it with sfl_part_*");
   SflCtl c = c_in;
   const size_t E = h->E, T = h->map.T;
   const int32_t cap = args ? args->stats_cap : 0;
@@ -478,6 +499,216 @@ int run(Handle<B>* h, const SflCtl& c_in, sfl_run_args* args) {
   for (void* p : scratch) h->be.free(p);
   if (rc) return fail(std::string("sfl_run: ") + h->be.error());
   return check_errors(h);
+}
+
+}  // namespace sfl
+
+namespace sfl {
+
+// ---------------------------------------------------------------------------
+// graph-partitioned mode (sfl_part.h): owned Q storage and one round's three steps
+// ---------------------------------------------------------------------------
+template <class B>
+int part_config(Handle<B>* h, int rank, int world, const int32_t* owner, uint32_t env_base, uint32_t E_tot,
+                uint32_t cap_req, uint32_t cap_upd) {
+  if (world < 1 || rank < 0 || rank >= world || world > 255) return fail("sfl_part_config: bad rank / world");
+  if (h->part.world) return fail("sfl_part_config: already configured");
+  if (env_base + h->E > E_tot) return fail("sfl_part_config: env range outside envs_total");
+  if (cap_req < h->E) return fail("sfl_part_config: request capacity must hold one request per local env");
+  if (cap_req >= (1u << 24) || cap_upd < 1) return fail("sfl_part_config: bad capacities");
+  const int S = h->map.S, K = h->map.K;
+  std::vector<int32_t> own(owner, owner + S);
+  for (int s = 0; s < S; ++s)
+    if (own[s] < 0 || own[s] >= world) return fail("sfl_part_config: owner out of range");
+  std::vector<uint64_t> qo(4 * (size_t)S, 0);
+  std::vector<uint32_t> ro(4 * (size_t)S, 0);
+  uint64_t off = 0;
+  uint32_t rows = 0;
+  for (int s = 0; s < S; ++s) {
+    if (own[s] != rank) continue;
+    const int P = h->h_sw_np[s];
+    for (int i = 0; i < P; ++i) {
+      const int g = 4 * s + i;
+      const uint32_t nrows = (uint32_t)(1u << P) * (uint32_t)K * 3u;
+      qo[g] = off;
+      ro[g] = rows;
+      off += (uint64_t)nrows * h->h_q_w[g];
+      rows += nrows;
+    }
+  }
+  // the env-local Q-table is not used in this mode: release it before the owned tables
+  h->be.sync();
+  h->dfree(h->st.q);
+  h->dfree(h->st.touched);
+  h->st.q = nullptr;
+  h->st.touched = nullptr;
+  SflPart& P = h->part;
+  P.rank = rank;
+  P.world = world;
+  P.env_base = env_base;
+  P.E_tot = E_tot;
+  P.cap_req = cap_req;
+  P.cap_upd = cap_upd;
+  P.q_own_per_env = off;
+  P.own_rows = rows;
+  P.own_words = (rows + 31u) / 32u;
+  P.owner = h->upload(own.data(), own.size());
+  P.q_off_own = h->upload(qo.data(), qo.size());
+  P.row_own = h->upload(ro.data(), ro.size());
+  P.q_own = h->template dalloc<double>((size_t)E_tot * (off ? off : 1));
+  P.touched_own = h->template dalloc<uint32_t>((size_t)E_tot * (P.own_words ? P.own_words : 1));
+  P.obs = h->template dalloc<Obs>(h->E);
+  P.req_ix = h->template dalloc<uint32_t>(h->E);
+  P.dec_done = h->template dalloc<int64_t>(h->E);
+  P.cnt = h->template dalloc<uint32_t>(2 * (size_t)world + 1);
+  if (!P.owner || !P.q_own || !P.touched_own || !P.obs || !P.req_ix || !P.dec_done || !P.cnt)
+    return fail("sfl_part_config: allocation failed (out of memory?)");
+  P.max_stage = P.cnt + 2 * world;
+  h->be.fill_f64(P.q_own, h->map.default_q, (size_t)E_tot * off);
+  h->be.memset(P.touched_own, 0, (size_t)E_tot * P.own_words * 4);
+  h->be.memset(P.dec_done, 0, h->E * 8);
+  // the partitioned rounds run the lane-per-env body: its (switch, train) slot layout
+  h->variant = 0;
+  return h->be.sync() ? fail(h->be.error()) : 0;
+}
+
+// Q-init patch rows on the owned blocks (sfl_apply_qinit for a partitioned handle)
+template <class B>
+int part_qinit(Handle<B>* h, uint32_t n_rows, const uint32_t* row_port, const uint32_t* row_state, const double* values) {
+  SflPart& P = h->part;
+  const int rank = P.rank;
+  std::vector<int32_t> own(h->map.S);
+  h->be.d2h(own.data(), P.owner, own.size() * 4);
+  if (h->be.sync()) return fail(h->be.error());
+  // apply on the host copy of one env's owned table, then replicate over all envs
+  std::vector<uint64_t> qo(4 * (size_t)h->map.S);
+  std::vector<uint32_t> ro(4 * (size_t)h->map.S);
+  h->be.d2h(qo.data(), P.q_off_own, qo.size() * 8);
+  h->be.d2h(ro.data(), P.row_own, ro.size() * 4);
+  if (h->be.sync()) return fail(h->be.error());
+  std::vector<double> tab(P.q_own_per_env, h->map.default_q);
+  std::vector<uint32_t> bits(P.own_words, 0u);
+  for (uint32_t r = 0; r < n_rows; ++r) {
+    const uint32_t g = row_port[r], st = row_state[r];
+    if (own[g >> 2] != rank) continue;
+    const int w = h->h_q_w[g];
+    for (int j = 0; j < w; ++j) {
+      const double v = values[(size_t)r * 4 + j];
+      tab[qo[g] + (size_t)st * w + j] = (v != v) ? h->map.default_q : v;
+    }
+    const uint32_t rid = ro[g] + st;
+    bits[rid >> 5] |= 1u << (rid & 31u);
+  }
+  // one env's owned table and key set, replicated over every env of the job
+  if (P.q_own_per_env) {
+    h->be.h2d(P.q_own, tab.data(), tab.size() * 8);
+    h->be.replicate(P.q_own, tab.size() * 8, P.E_tot);
+  }
+  if (P.own_words) {
+    h->be.h2d(P.touched_own, bits.data(), bits.size() * 4);
+    h->be.replicate(P.touched_own, bits.size() * 4, P.E_tot);
+  }
+  return h->be.sync() ? fail(h->be.error()) : 0;
+}
+
+// one env of the job (global index): its owned Q blocks in the full per-env layout (other
+// entries untouched) and its owned key-set bits OR-ed into `touched`
+template <class B>
+int part_get_q(Handle<B>* h, uint32_t genv, double* q, uint32_t* touched) {
+  SflPart& P = h->part;
+  if (genv >= P.E_tot) return fail("sfl_part_get_q: env out of range");
+  std::vector<int32_t> own(h->map.S);
+  std::vector<uint64_t> qo(4 * (size_t)h->map.S);
+  std::vector<uint32_t> ro(4 * (size_t)h->map.S);
+  std::vector<double> tab(P.q_own_per_env);
+  std::vector<uint32_t> bits(P.own_words);
+  h->be.d2h(own.data(), P.owner, own.size() * 4);
+  h->be.d2h(qo.data(), P.q_off_own, qo.size() * 8);
+  h->be.d2h(ro.data(), P.row_own, ro.size() * 4);
+  if (P.q_own_per_env) h->be.d2h(tab.data(), P.q_own + (size_t)genv * P.q_own_per_env, tab.size() * 8);
+  if (P.own_words) h->be.d2h(bits.data(), P.touched_own + (size_t)genv * P.own_words, bits.size() * 4);
+  if (h->be.sync()) return fail(h->be.error());
+  const int K = h->map.K;
+  for (int s = 0; s < h->map.S; ++s) {
+    if (own[s] != P.rank) continue;
+    const int np = h->h_sw_np[s];
+    for (int i = 0; i < np; ++i) {
+      const int g = 4 * s + i;
+      const uint32_t nrows = (uint32_t)(1u << np) * (uint32_t)K * 3u;
+      const int w = h->h_q_w[g];
+      if (q) memcpy(q + h->h_q_off[g], tab.data() + qo[g], (size_t)nrows * w * 8);
+      if (touched)
+        for (uint32_t r = 0; r < nrows; ++r) {
+          const uint32_t lr = ro[g] + r;
+          if ((bits[lr >> 5] >> (lr & 31u)) & 1u) {
+            const uint32_t fr = h->h_row_base[g] + r;
+            touched[fr >> 5] |= 1u << (fr & 31u);
+          }
+        }
+    }
+  }
+  return 0;
+}
+
+template <class B>
+int part_begin(Handle<B>* h) {
+  if (!h->part.world) return fail("sfl_part_begin: handle not partitioned");
+  h->be.memset(h->part.dec_done, 0, h->E * 8);
+  return h->be.sync() ? fail(h->be.error()) : 0;
+}
+
+// local step of a round: every env applies its reply, runs to its next decision and emits the
+// request (and the update records of its post step)
+template <class B>
+int part_local(Handle<B>* h, int64_t budget, const void* rep_in, void* req_out, void* upd_out, uint64_t* n_req) {
+  SflPart& P = h->part;
+  if (!P.world) return fail("sfl_part_local: handle not partitioned");
+  P.rep_in = (const PartRep*)rep_in;
+  P.req_out = (PartReq*)req_out;
+  P.upd_out = (PartUpd*)upd_out;
+  h->be.memset(P.cnt, 0, (2 * (size_t)P.world + 1) * 4);
+  SflCtl c{};
+  c.mode = 0;
+  c.ep_target = -1;
+  c.dec_budget = budget;
+  c.launch_dec = h->d_launch_dec;
+  c.launch_ticks = h->d_launch_ticks;
+  c.launch_bytes = h->d_launch_bytes;
+  float ms = 0.f;
+  int rc = h->be.part_local(h->map, h->st, c, P, &ms);
+  h->last_kernel_ms = ms;
+  std::vector<uint32_t> cnt(2 * (size_t)P.world + 1);
+  h->be.d2h(cnt.data(), P.cnt, cnt.size() * 4);
+  if (!rc) rc = h->be.sync();
+  if (rc) return fail(std::string("sfl_part_local: ") + h->be.error());
+  uint64_t n = 0;
+  for (int g = 0; g < P.world; ++g) n += cnt[g];
+  if (n_req) *n_req = n;
+  return check_errors(h);
+}
+
+template <class B>
+int part_answer(Handle<B>* h, const void* req_in, void* rep_out) {
+  SflPart& P = h->part;
+  if (!P.world) return fail("sfl_part_answer: handle not partitioned");
+  h->be.part_answer(h->map, P, (const PartReq*)req_in, (PartRep*)rep_out);
+  return h->be.sync() ? fail(std::string("sfl_part_answer: ") + h->be.error()) : 0;
+}
+
+template <class B>
+int part_update(Handle<B>* h, const void* upd_in) {
+  SflPart& P = h->part;
+  if (!P.world) return fail("sfl_part_update: handle not partitioned");
+  const PartUpd* in = (const PartUpd*)upd_in;
+  uint32_t max_stage = 0;
+  for (int g = 0; g < P.world; ++g) {
+    PartUpd hd;
+    h->be.d2h(&hd, in + (size_t)g * (P.cap_upd + 1), sizeof hd);
+    if (h->be.sync()) return fail(h->be.error());
+    if (hd.genv > 0 && hd.state > max_stage) max_stage = hd.state;
+  }
+  for (uint32_t st = 0; st <= max_stage; ++st) h->be.part_update(h->map, P, in, (int)st);
+  return h->be.sync() ? fail(std::string("sfl_part_update: ") + h->be.error()) : 0;
 }
 
 }  // namespace sfl

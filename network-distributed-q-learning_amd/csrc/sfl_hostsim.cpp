@@ -55,6 +55,37 @@ struct HostBackend {
     return 0;
   }
   int sync() { return 0; }
+  void replicate(void* base, size_t bytes, uint32_t n) {
+    for (uint32_t i = 1; i < n; ++i) memcpy((char*)base + (size_t)i * bytes, base, bytes);
+  }
+  int part_local(const sfl::SflMap& m, const sfl::SflState& s, const sfl::SflCtl& c, const sfl::SflPart& P, float* ms) {
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int64_t e = 0; e < (int64_t)s.E; ++e) {
+      if (m.T <= 32) sfl::env_run_part<1>(m, s, c, P, (uint32_t)e);
+      else if (m.T <= 64) sfl::env_run_part<2>(m, s, c, P, (uint32_t)e);
+      else sfl::env_run_part<4>(m, s, c, P, (uint32_t)e);
+    }
+    for (int g = 0; g < P.world; ++g) sfl::part_headers(P, g);
+    *ms = 0.f;
+    return 0;
+  }
+  void part_answer(const sfl::SflMap& m, const sfl::SflPart& P, const sfl::PartReq* in, sfl::PartRep* out) {
+    for (int g = 0; g < P.world; ++g) {
+      const size_t base = (size_t)g * (P.cap_req + 1);
+      const int64_t n = in[base].genv;
+#pragma omp parallel for
+      for (int64_t k = 1; k <= n; ++k) sfl::part_answer_one(m, P, in[base + k], out[base + k]);
+    }
+  }
+  void part_update(const sfl::SflMap& m, const sfl::SflPart& P, const sfl::PartUpd* in, int stage) {
+    for (int g = 0; g < P.world; ++g) {
+      const size_t base = (size_t)g * (P.cap_upd + 1);
+      const int64_t n = in[base].genv;
+#pragma omp parallel for
+      for (int64_t k = 1; k <= n; ++k)
+        if (in[base + k].stage == stage) sfl::part_update_one(m, P, in[base + k]);
+    }
+  }
 };
 
 }  // namespace

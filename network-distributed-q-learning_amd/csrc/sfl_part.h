@@ -1,0 +1,315 @@
+// Graph-partitioned mode (BASELINE.json configs[4], SURVEY.md §8(e) "C5"): the switch agents
+// are partitioned over the ranks, and each rank stores the Q rows of the switches it owns,
+// for every env of the job.  Envs are sharded over the ranks as in the env-sharded mode; an
+// env's decision at switch s asks owner(s) for the Q row (argmax and max), and its post step
+// sends the Q update of the pending (switch, train) entry -- the bootstrap from the successor
+// agent's row, distr_q.py:419-447 -- to owner(previous switch).  That is the reference's
+// network-distributed learner with the successor-Q values crossing GPU boundaries.
+//
+// One round = every local env makes (at most) one decision:
+//   local    (env_run_part): apply the reply of the previous round's request, continue the
+//            env (post, ticks, episode ends) up to the next decision, observe it and emit its
+//            request; post steps emit update records
+//   exchange updates + requests (RCCL all-to-all; segment per destination rank)
+//   update   (part_update_one): the owner applies the updates, stage by stage
+//   answer   (part_answer_one): the owner computes max(row) and the masked argmax
+//   exchange replies (the same segment layout, back to the requesters)
+// Each env's own sequence of operations is that of env_run (sfl_core.h), so the results are
+// bit-identical to the fused kernels (tests/test_partition.py).
+#pragma once
+#include "sfl_core.h"
+
+namespace sfl {
+
+enum : uint32_t { F_REQ = 64 };  // eflags: a request is waiting for its reply
+enum : uint32_t { E_MSG_OVF = 16 };  // a message segment overflowed (capacity too small)
+
+// message records; record 0 of each destination segment is a header whose first word is the
+// number of records that follow
+struct PartReq {
+  uint32_t genv;   // global env index
+  uint16_t port;   // 4 * switch + in-port slot (the row's block)
+  uint16_t amask;  // allowed actions (get_action_mask)
+  uint32_t state;  // observation state index within the block
+  uint32_t flags;  // 1: exploratory action (no argmax, no key-set insert)
+};
+struct PartRep {
+  int32_t action;  // masked argmax (distr_q.py:468-490); -1 for exploratory requests
+  int32_t pad;
+  double mq;       // max over the full row (distr_q.py:449-466)
+};
+struct PartUpd {
+  uint32_t genv;
+  uint16_t port;
+  uint8_t j;      // compact column
+  uint8_t stage;  // 0: pending update / key-set inserts; 1 + i: bonus of the i-th arrived train
+  uint32_t state;
+  uint32_t kind;  // 0: q <- (1 - lr) q + lr target;  1: key-set insert only
+  double lr;
+  double target;
+};
+static_assert(sizeof(PartReq) == 16 && sizeof(PartRep) == 16 && sizeof(PartUpd) == 32, "record sizes");
+
+struct SflPart {
+  int32_t rank, world;
+  uint32_t env_base;  // global index of local env 0
+  uint32_t E_tot;     // envs over all ranks
+  uint32_t cap_req, cap_upd;  // records per destination segment (without the header)
+  uint64_t q_own_per_env;     // doubles of owned Q per env
+  uint32_t own_rows, own_words;
+  const int32_t* owner;       // [S] rank owning each switch agent
+  const uint64_t* q_off_own;  // [4S] block offset in the owned table (owned switches only)
+  const uint32_t* row_own;    // [4S] first owned row id of the block
+  double* q_own;              // [E_tot][q_own_per_env]
+  uint32_t* touched_own;      // [E_tot][own_words]
+  Obs* obs;                   // [E] observation waiting for its reply
+  uint32_t* req_ix;           // [E] destination << 24 | record index of that request
+  int64_t* dec_done;          // [E] decisions since sfl_part_begin
+  uint32_t* cnt;              // [2][world] records emitted this round (requests, updates)
+  uint32_t* max_stage;        // [1] highest update stage emitted this round
+  // round buffers (set per call)
+  const PartRep* rep_in;      // [world][cap_req + 1]
+  PartReq* req_out;           // [world][cap_req + 1]
+  PartUpd* upd_out;           // [world][cap_upd + 1]
+};
+
+SFL_FN uint32_t fetch_add_u32(uint32_t* p, uint32_t v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return atomicAdd(p, v);
+#else
+  return __atomic_fetch_add(p, v, __ATOMIC_RELAXED);
+#endif
+}
+SFL_FN void fetch_or_u32(uint32_t* p, uint32_t v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  atomicOr(p, v);
+#else
+  __atomic_fetch_or(p, v, __ATOMIC_RELAXED);
+#endif
+}
+SFL_FN void fetch_max_u32(uint32_t* p, uint32_t v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  atomicMax(p, v);
+#else
+  uint32_t cur = __atomic_load_n(p, __ATOMIC_RELAXED);
+  while (cur < v && !__atomic_compare_exchange_n(p, &cur, v, true, __ATOMIC_RELAXED, __ATOMIC_RELAXED)) {
+  }
+#endif
+}
+
+// the post step's Q operations as update records to the owner of the row's switch
+template <class V>
+struct MsgQ {
+  V& v;
+  const SflPart& P;
+  uint32_t genv;
+  double mq;  // max of the decision's own row, from the owner's reply
+  SFL_FN void emit(int sw, int slot, uint32_t state, int j, uint32_t kind, double lr, double target, int stage) {
+    const int dst = P.owner[sw];
+    const uint32_t k = fetch_add_u32(&P.cnt[P.world + dst], 1u);
+    if (k >= P.cap_upd) {
+      v.err |= E_MSG_OVF;
+      return;
+    }
+    PartUpd& u = P.upd_out[(size_t)dst * (P.cap_upd + 1) + 1 + k];
+    u.genv = genv;
+    u.port = (uint16_t)(4 * sw + slot);
+    u.j = (uint8_t)j;
+    u.stage = (uint8_t)stage;
+    u.state = state;
+    u.kind = kind;
+    u.lr = lr;
+    u.target = target;
+    if (stage > 0) fetch_max_u32(P.max_stage, (uint32_t)stage);
+  }
+  SFL_FN void touch(int sw, int slot, uint32_t state) { emit(sw, slot, state, 0, 1u, 0.0, 0.0, 0); }
+  SFL_FN double row_max_of(const Decision&) { return mq; }
+  SFL_FN void update(int ps, int pslot, uint32_t pstate, int pj, double lr, double target, int stage) {
+    emit(ps, pslot, pstate, pj, 0u, lr, target, stage);
+  }
+};
+
+// the map as row_max / max_action see it
+struct MapView {
+  const SflMap& m;
+};
+
+// owner side: one request -> reply (distr_q.py:449-490 on the owned row)
+SFL_FN void part_answer_one(const SflMap& m, const SflPart& P, const PartReq& r, PartRep& out) {
+  const int port = r.port, sw = port >> 2, slot = port & 3;
+  const double* row = P.q_own + (size_t)r.genv * P.q_own_per_env + P.q_off_own[port] + (size_t)r.state * m.q_w[port];
+  const MapView mv{m};
+  out.mq = row_max(mv, sw, slot, row);
+  out.pad = 0;
+  if (r.flags & 1u) {
+    out.action = -1;
+  } else {
+    const uint32_t rid = P.row_own[port] + r.state;
+    fetch_or_u32(&P.touched_own[(size_t)r.genv * P.own_words + (rid >> 5)], 1u << (rid & 31u));
+    out.action = max_action(mv, sw, slot, row, r.amask);
+  }
+}
+
+// owner side: one update record of the given stage
+SFL_FN void part_update_one(const SflMap& m, const SflPart& P, const PartUpd& u) {
+  const int port = u.port;
+  const uint32_t rid = P.row_own[port] + u.state;
+  fetch_or_u32(&P.touched_own[(size_t)u.genv * P.own_words + (rid >> 5)], 1u << (rid & 31u));
+  if (u.kind == 0u) {
+    double* q = P.q_own + (size_t)u.genv * P.q_own_per_env + P.q_off_own[port] + (size_t)u.state * m.q_w[port] + u.j;
+    const double a = (1.0 - u.lr) * *q;
+    const double bb = u.lr * u.target;
+    *q = a + bb;
+  }
+}
+
+// local side: one env for one round (env_run of sfl_core.h, with the Q row operations sent to
+// their owners).  Stops after emitting the next decision's request, or when the env has made
+// its decisions for this part_step (c.dec_budget) or reached its episode target.
+template <int NW>
+SFL_FN void env_run_part(const SflMap& m, const SflState& s, const SflCtl& c, const SflPart& P, uint32_t e) {
+  using V = Env<NW>;
+  V v(m, s, e);
+  v.flags = s.eflags[e];
+  v.now = s.elapsed[e];
+  v.epoch = s.epoch[e];
+  v.err = s.err[e];
+  int32_t phase = s.phase[e];
+  int64_t dec = P.dec_done[e];
+  uint64_t ticks = 0, abytes = 0, ndec = 0;
+  Decision d;
+  d.sw = d.h = d.slot = d.action = d.j = d.reward = d.next_sw = 0;
+  d.state = 0;
+  double mq_cur = 0.0;
+  double cum = s.cum_reward[e];
+  const bool test_mode = c.mode == 1;
+  const uint32_t genv = P.env_base + e;
+  v.masks_load();
+  while (true) {
+    if (phase == PH_RESET) {
+      if (test_mode) {
+        if (c.ep_target >= 0 && s.n_test[e] >= c.ep_target) break;
+        v.flags |= F_GREEDY;
+      } else {
+        if (c.ep_target >= 0 && s.ep_t[e] >= c.ep_target) break;
+        const int32_t t = s.ep_t[e];
+        if (c.exploit_freq > 0 && (t + 1) % c.exploit_freq == 0 && !(v.flags & F_EXPLOIT_DONE)) v.flags |= F_GREEDY;
+        else v.flags &= ~F_GREEDY;
+      }
+      env_reset(v);
+      cum = 0.0;
+      phase = PH_TICK;
+    } else if (phase == PH_TICK) {
+      int live = m.T;
+#pragma unroll
+      for (int w = 0; w < V::kNW; ++w) live -= popc32(v.msk[1][w]);
+      abytes += 36ull * (uint64_t)live;
+      env_tick(v);
+      ticks++;
+      if (v.flags & F_TERM) phase = (v.flags & F_INFLIGHT) ? PH_POST : PH_END;
+      else if (!queue_empty(v)) phase = (v.flags & F_INFLIGHT) ? PH_POST : PH_DECIDE;
+    } else if (phase == PH_DECIDE || phase == PH_POST) {
+      bool post_now = phase == PH_POST;
+      if (phase == PH_DECIDE) {
+        const bool greedy = (v.flags & F_GREEDY) != 0;
+        if (!(v.flags & F_REQ)) {
+          if (c.dec_budget > 0 && dec >= c.dec_budget) break;
+          Obs o;
+          decide_observe(v, o, greedy);
+          const int dst = P.owner[o.sw];
+          const uint32_t k = fetch_add_u32(&P.cnt[dst], 1u);
+          if (k >= P.cap_req) {
+            v.err |= E_MSG_OVF;
+            break;
+          }
+          PartReq& r = P.req_out[(size_t)dst * (P.cap_req + 1) + 1 + k];
+          r.genv = genv;
+          r.port = (uint16_t)(4 * o.sw + o.slot);
+          r.amask = (uint16_t)o.amask;
+          r.state = o.state;
+          r.flags = o.explore ? 1u : 0u;
+          P.obs[e] = o;
+          P.req_ix[e] = ((uint32_t)dst << 24) | (1u + k);
+          v.flags |= F_REQ;
+          break;  // the round ends here: the owner answers before this env goes on
+        }
+        v.flags &= ~F_REQ;
+        const Obs o = P.obs[e];
+        const uint32_t ix = P.req_ix[e];
+        const PartRep& rp = P.rep_in[(size_t)(ix >> 24) * (P.cap_req + 1) + (ix & 0xFFFFFFu)];
+        mq_cur = rp.mq;
+        decide_apply(v, o, o.explore ? o.action : rp.action, d);
+        abytes += 220ull + 48ull * m.sw_np[d.sw] + 8ull * m.sw_na[d.sw];
+        v.flags |= F_INFLIGHT;
+        if (queue_empty(v)) phase = PH_TICK;  // ticks happen between the step and the update
+        else post_now = true;
+      }
+      if (post_now) {
+        if (!(v.flags & F_GREEDY)) {
+          MsgQ<V> q{v, P, genv, mq_cur};
+          env_post(v, d, q);
+        }
+        v.flags &= ~F_INFLIGHT;
+        cum += (double)d.reward;
+        s.ep_dec[e] += 1;
+        s.dec_total[e] += 1;
+        s.step_ctr[e] += 1;
+        if (s.step_ctr[e] > m.max_steps) v.flags |= F_TRUNC;
+        dec++;
+        ndec++;
+        phase = (v.flags & (F_TERM | F_TRUNC)) ? PH_END : PH_DECIDE;
+        if (c.dec_budget > 0 && dec >= c.dec_budget) break;
+      }
+    } else {  // PH_END
+      int arrived = 0;
+#pragma unroll
+      for (int w = 0; w < V::kNW; ++w) arrived += popc32(v.msk[1][w]);
+      const size_t cap = (size_t)(c.stats_cap > 0 ? c.stats_cap : 1);
+      const bool greedy = (v.flags & F_GREEDY) != 0;
+      if (c.st_cum && c.stats_cap > 0 && (!greedy || test_mode)) {
+        const int32_t i = (greedy && test_mode) ? s.n_test[e] : s.ep_t[e];
+        const size_t row = (size_t)(i - c.stats_base) % cap;
+        c.st_cum[row * s.E + e] = cum;
+        c.st_arrived[row * s.E + e] = arrived;
+        c.st_mf[row * s.E + e] = s.n_mf[e];
+        c.st_dec[row * s.E + e] = s.ep_dec[e];
+        c.st_ticks[row * s.E + e] = s.ep_ticks[e];
+        for (int h = 0; h < m.T; ++h) c.st_delays[(row * m.T + h) * s.E + e] = s.tr_delay[v.ix(h)];
+      }
+      if (greedy && !test_mode && c.sx_cum && c.stats_cap > 0) {
+        const size_t row = (size_t)(s.ep_t[e] - c.stats_base) % cap;
+        c.sx_cum[row * s.E + e] = cum;
+        c.sx_arrived[row * s.E + e] = arrived;
+      }
+      if (greedy) {
+        if (test_mode) s.n_test[e] += 1;
+        else v.flags |= F_EXPLOIT_DONE;
+      } else {
+        s.ep_t[e] += 1;
+        v.flags &= ~F_EXPLOIT_DONE;
+      }
+      phase = PH_RESET;
+    }
+  }
+  v.masks_store();
+  s.phase[e] = phase;
+  s.elapsed[e] = v.now;
+  s.eflags[e] = v.flags;
+  s.epoch[e] = v.epoch;
+  s.err[e] = v.err;
+  s.cum_reward[e] = cum;
+  P.dec_done[e] = dec;
+  if (c.launch_dec) c.launch_dec[e] = ndec;
+  if (c.launch_ticks) c.launch_ticks[e] = ticks;
+  if (c.launch_bytes) c.launch_bytes[e] = abytes;
+}
+
+// write the record counts into the segment headers (after the local kernel)
+SFL_FN void part_headers(const SflPart& P, int dst) {
+  const uint32_t nr = P.cnt[dst], nu = P.cnt[P.world + dst];
+  P.req_out[(size_t)dst * (P.cap_req + 1)].genv = nr < P.cap_req ? nr : P.cap_req;
+  P.upd_out[(size_t)dst * (P.cap_upd + 1)].genv = nu < P.cap_upd ? nu : P.cap_upd;
+  P.upd_out[(size_t)dst * (P.cap_upd + 1)].state = *P.max_stage;
+}
+
+}  // namespace sfl

@@ -1,0 +1,172 @@
+"""Graph-partitioned SwitchFL learner (BASELINE.json configs[4], SURVEY.md §8(e) "C5").
+
+The reference's learner is a network of switch agents: each switch keeps its own Q-table
+(the dict partitioned by the switch coordinates, distr_q.py:47-57) and bootstraps from the
+*successor* agent's row, ``max_q(next_state, next_agent)`` (distr_q.py:419-466).  Here the
+switch agents are partitioned over the ranks (one process per GPU): rank r owns the Q rows of
+its switches for every env of the job and answers the row lookups for them; envs are sharded
+over the ranks as in the env-sharded mode.  Each round every env makes one decision:
+
+    sfl_part_local    apply last round's reply, run to the next decision, emit its request
+                      (and the update records of the post step)
+    all-to-all        update + request buffers  (RCCL over xGMI: torch.distributed "nccl")
+    sfl_part_update   owner applies the bootstrapped updates (stage-ordered)
+    sfl_part_answer   owner: max over the row + masked argmax
+    all-to-all        replies back
+
+Every env performs exactly the operations of the fused kernels in the same order, so the
+results are bit-identical to the single-process run (tests/test_partition.py).  Message
+buffers are fixed [world][cap + 1] record segments whose first record carries the count, so a
+round needs no host-side split sizes.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from collections import deque
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+from . import _lib
+from .compiler import CompiledMap
+from .runtime import Batch, _ptr
+
+
+def partition_switches(cm: CompiledMap, world: int) -> np.ndarray:
+    """owner[S]: contiguous blocks of a breadth-first order of the switch graph, so most rail
+    edges (successor lookups) stay inside one rank."""
+    S = cm.S
+    nb = np.asarray(cm.arrays["port_nb"]).reshape(S, 4)
+    adj = [sorted({int(p) >> 2 for p in nb[s] if p >= 0} - {s}) for s in range(S)]
+    order: List[int] = []
+    seen = [False] * S
+    for s0 in range(S):
+        if seen[s0]:
+            continue
+        seen[s0] = True
+        dq = deque([s0])
+        while dq:
+            s = dq.popleft()
+            order.append(s)
+            for t in adj[s]:
+                if not seen[t]:
+                    seen[t] = True
+                    dq.append(t)
+    owner = np.zeros(S, np.int32)
+    for i, s in enumerate(order):
+        owner[s] = i * world // S
+    return owner
+
+
+def cut_fraction(cm: CompiledMap, owner: np.ndarray) -> float:
+    """Fraction of switch-to-switch rail edges whose ends have different owners."""
+    nb = np.asarray(cm.arrays["port_nb"]).reshape(cm.S, 4)
+    e = c = 0
+    for s in range(cm.S):
+        for p in nb[s]:
+            if p >= 0 and (int(p) >> 2) != s:
+                e += 1
+                c += int(owner[int(p) >> 2] != owner[s])
+    return c / max(1, e)
+
+
+class PartitionedBatch:
+    """This rank's envs + its switch agents' Q rows.  ``dist``: torch.distributed (or None for one rank);
+    ``device``: a torch device for the message buffers ("cuda" for the HIP library, "cpu" for the host build)."""
+
+    def __init__(self, cm: CompiledMap, hp: dict, seeds: Sequence[int], env_base: int, envs_total: int,
+                 rank: int = 0, world: int = 1, dist=None, lib: Optional[_lib.Lib] = None, device: int = 0,
+                 owner: Optional[np.ndarray] = None, upd_per_env: int = 8, ntab: Optional[int] = None,
+                 buffer_device: str = "cuda"):
+        import torch
+        self.torch = torch
+        kw = {} if ntab is None else dict(ntab=ntab)
+        self.batch = Batch(cm, hp, seeds, lib=lib, device=device, **kw)
+        self.lib = self.batch.lib
+        self.cm, self.rank, self.world, self.dist = cm, int(rank), int(world), dist
+        self.E = self.batch.E
+        self.env_base, self.envs_total = int(env_base), int(envs_total)
+        self.owner = np.ascontiguousarray(owner if owner is not None else partition_switches(cm, world), np.int32)
+        self.cap_req = self.E
+        self.cap_upd = max(64, upd_per_env * self.E)
+        self.lib.check(self.lib.dll.sfl_part_config(self.batch.h, self.rank, self.world, _ptr(self.owner, C.c_int32),
+                                                    self.env_base, self.envs_total, self.cap_req, self.cap_upd),
+                       "sfl_part_config")
+        rq, rp, up = C.c_uint32(), C.c_uint32(), C.c_uint32()
+        self.lib.dll.sfl_part_record_sizes(C.byref(rq), C.byref(rp), C.byref(up))
+        dev = torch.device(buffer_device)
+        nreq = self.world * (self.cap_req + 1) * rq.value
+        nrep = self.world * (self.cap_req + 1) * rp.value
+        nupd = self.world * (self.cap_upd + 1) * up.value
+        z = lambda n: torch.zeros(n, dtype=torch.uint8, device=dev)  # noqa: E731
+        self.req_send, self.req_recv = z(nreq), z(nreq)
+        self.rep_send, self.rep_recv = z(nrep), z(nrep)
+        self.upd_send, self.upd_recv = z(nupd), z(nupd)
+        self.on_gpu = dev.type == "cuda"
+        self.rounds = 0
+
+    def close(self):
+        self.batch.close()
+
+    # ---- the reference's learn() set-up, on the partitioned tables ----------------------------
+    def learn_begin(self):
+        self.batch.learn_begin()
+
+    def apply_qinit(self):
+        self.batch.apply_qinit()
+
+    # ---- one part step: every env makes `decisions_per_env` decisions ---------------------------
+    def _exchange(self, recv, send):
+        if self.dist is None or self.world == 1:
+            recv.copy_(send)
+        else:
+            self.dist.all_to_all_single(recv, send)
+        if self.on_gpu:
+            self.torch.cuda.current_stream().synchronize()
+
+    def step(self, decisions_per_env: int) -> int:
+        """Advance every local env by ``decisions_per_env`` learning decisions (the sfl_step contract);
+        returns the number of rounds.  Collective over the ranks."""
+        d = self.lib.dll
+        h = self.batch.h
+        ptr = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
+        self.lib.check(d.sfl_part_begin(h), "sfl_part_begin")
+        rounds = 0
+        for _ in range(int(decisions_per_env) + 1):
+            n = C.c_uint64(0)
+            self.lib.check(d.sfl_part_local(h, int(decisions_per_env), ptr(self.rep_recv), ptr(self.req_send),
+                                            ptr(self.upd_send), C.byref(n)), "sfl_part_local")
+            self._exchange(self.upd_recv, self.upd_send)
+            self._exchange(self.req_recv, self.req_send)
+            self.lib.check(d.sfl_part_update(h, ptr(self.upd_recv)), "sfl_part_update")
+            self.lib.check(d.sfl_part_answer(h, ptr(self.req_recv), ptr(self.rep_send)), "sfl_part_answer")
+            self._exchange(self.rep_recv, self.rep_send)
+            rounds += 1
+        if n.value != 0:
+            raise _lib.SflError(f"rank {self.rank}: {n.value} requests still open after the last round")
+        self.rounds += rounds
+        return rounds
+
+    # ---- owned Q blocks (assembled over ranks by the caller) --------------------------------------
+    def owned_q(self, global_env: int):
+        """(q, touched) in the full per-env layout: this rank's owned blocks, NaN elsewhere."""
+        q = np.full(self.cm.q_per_env, np.nan)
+        t = np.zeros((self.cm.rows_per_env + 31) // 32, np.uint32)
+        self.lib.check(self.lib.dll.sfl_part_get_q(self.batch.h, int(global_env), _ptr(q, C.c_double),
+                                                   _ptr(t, C.c_uint32)), "sfl_part_get_q")
+        return q, t
+
+    def owned_mask(self) -> np.ndarray:
+        """Boolean mask over the full per-env Q layout: entries of switches this rank owns."""
+        cm = self.cm
+        A = cm.arrays
+        mk = np.zeros(cm.q_per_env, bool)
+        for s in range(cm.S):
+            if self.owner[s] != self.rank:
+                continue
+            P_ = len(cm.ports[s])
+            for slot in range(P_):
+                g = 4 * s + slot
+                n = (1 << P_) * cm.K * 3 * int(A["q_w"][g])
+                mk[int(A["q_off"][g]):int(A["q_off"][g]) + n] = True
+        return mk

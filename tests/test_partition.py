@@ -1,0 +1,139 @@
+"""Graph-partitioned mode (BASELINE.json configs[4]; network-distributed-q-learning_amd/partition.py)
+on the host build of the kernel body: the switch agents' Q rows live on their owner rank and the
+row lookups / bootstrapped updates travel as all-to-all messages, yet every env's Q-table, key
+set and env state are bit-identical to the fused single-process run (distr_q.py:419-466 evaluated
+across ranks).  World size 2 runs on gloo."""
+import ctypes as C
+import importlib
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from tests import hostsim
+
+HP = dict(gamma=1.0, epsilon=0.5, epsilon_decay_rate=0.9997, lr=0.1, lr_decay_rate=1.0, default_q=0.0)
+mapgen = importlib.import_module("network-distributed-q-learning_amd.mapgen")
+comp = importlib.import_module("network-distributed-q-learning_amd.compiler")
+runtime = importlib.import_module("network-distributed-q-learning_amd.runtime")
+part = importlib.import_module("network-distributed-q-learning_amd.partition")
+
+
+def _env_state(b, env):
+    cm = b.cm
+    el, ph = C.c_int32(), C.c_int32()
+    sem = np.zeros(4 * cm.S, np.uint64)
+    pos = np.zeros(cm.T, np.int32)
+    bits = np.zeros(cm.T, np.uint32)
+    P = C.POINTER
+    b.lib.check(b.lib.dll.sfl_get_env_state(b.h, env, C.byref(el), C.byref(ph), sem.ctypes.data_as(P(C.c_uint64)),
+                                            pos.ctypes.data_as(P(C.c_int32)), bits.ctypes.data_as(P(C.c_uint32))),
+                "sfl_get_env_state")
+    return el.value, ph.value, sem, pos, bits
+
+
+def _fused(cm, seeds, steps):
+    ref = runtime.Batch(cm, HP, seeds, lib=hostsim.lib(), ntab=4096)
+    ref.learn_begin()
+    ref.apply_qinit()
+    for n in steps:
+        ref.step(n)
+    return ref
+
+
+def _check_rank(pb, ref, local_ids):
+    mk = pb.owned_mask()
+    A = pb.cm.arrays
+    own_rows = np.zeros(pb.cm.rows_per_env, bool)
+    for s in range(pb.cm.S):
+        if pb.owner[s] != pb.rank:
+            continue
+        for slot in range(len(pb.cm.ports[s])):
+            g = 4 * s + slot
+            base, n = int(A["row_base"][g]), (1 << len(pb.cm.ports[s])) * pb.cm.K * 3
+            own_rows[base:base + n] = True
+    for ge in range(pb.envs_total):
+        q, t = pb.owned_q(ge)
+        qr, tr = ref.q_raw(ge)
+        assert np.array_equal(q[mk], qr[mk]), ("q", pb.rank, ge)
+        assert np.isnan(q[~mk]).all()
+        bits = np.unpackbits(t.view(np.uint8), bitorder="little")[:pb.cm.rows_per_env].astype(bool)
+        rbits = np.unpackbits(tr.view(np.uint8), bitorder="little")[:pb.cm.rows_per_env].astype(bool)
+        assert np.array_equal(bits, rbits & own_rows), ("touched", pb.rank, ge)
+    for le, ge in enumerate(local_ids):
+        a, b_ = _env_state(pb.batch, le), _env_state(ref, ge)
+        assert a[0] == b_[0] and a[1] == b_[1]
+        for x, y in zip(a[2:], b_[2:]):
+            assert np.array_equal(x, y)
+
+
+@pytest.mark.parametrize("cfg", ["c2", "c5"])
+def test_single_rank_partition_matches_fused(cfg):
+    cm = comp.compile_scenario(mapgen.make_config(cfg))
+    seeds = [450565 + i for i in range(4)]
+    pb = part.PartitionedBatch(cm, HP, seeds, 0, 4, lib=hostsim.lib(), ntab=4096, buffer_device="cpu")
+    pb.learn_begin()
+    pb.apply_qinit()
+    for n in (70, 130):
+        assert pb.step(n) == n + 1
+    _check_rank(pb, _fused(cm, seeds, (70, 130)), range(4))
+
+
+def test_partition_switches_balanced_and_local():
+    cm = comp.compile_scenario(mapgen.make_config("c5"))
+    own = part.partition_switches(cm, 8)
+    counts = np.bincount(own, minlength=8)
+    assert counts.sum() == cm.S and counts.max() - counts.min() <= 1
+    # BFS blocks keep most successor lookups on the owning rank: less than half the cut of s mod 8
+    assert part.cut_fraction(cm, own) < 0.5 * part.cut_fraction(cm, np.arange(cm.S, dtype=np.int32) % 8)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, cfg, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world), RANK=str(rank),
+                          LOCAL_RANK=str(rank))
+        par = importlib.import_module("network-distributed-q-learning_amd.parallel")
+        dist = par.init("gloo")
+        cm = comp.compile_scenario(mapgen.make_config(cfg))
+        e_loc = 3
+        seeds = par.shard_seeds(450565, e_loc, rank)
+        pb = part.PartitionedBatch(cm, HP, seeds, rank * e_loc, world * e_loc, rank=rank, world=world, dist=dist,
+                                   lib=hostsim.lib(), ntab=4096, buffer_device="cpu")
+        pb.learn_begin()
+        pb.apply_qinit()
+        for n in (90, 60):
+            pb.step(n)
+        ref = _fused(cm, [450565 + i for i in range(world * e_loc)], (90, 60))
+        _check_rank(pb, ref, range(rank * e_loc, (rank + 1) * e_loc))
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, "ok"))
+    except Exception as ex:  # report to the parent instead of hanging it
+        q.put((rank, repr(ex)))
+        raise
+
+
+@pytest.mark.parametrize("cfg", ["c2", "c5"])
+def test_two_rank_partition_matches_fused(cfg):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, cfg, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=600) for _ in range(2))
+    for p in procs:
+        p.join(timeout=120)
+    assert res == [(0, "ok"), (1, "ok")], res
+    for p in procs:
+        assert p.exitcode == 0
