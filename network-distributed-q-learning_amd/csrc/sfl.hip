@@ -34,10 +34,10 @@ __global__ void __launch_bounds__(256) k_run(const sfl::SflMap* __restrict__ m, 
 
 // One env per wavefront (sfl_wave.h): 4 envs per block.  PPL / SPL = semaphore / counter
 // registers per lane (sfl::kVariants).
-template <int PPL, int SPL>
+template <int PPL, int SPL, int TW>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SFL_WAVE_OCC))) k_wave(const sfl::SflMap* __restrict__ m, const sfl::SflState* __restrict__ s,
                                               const sfl::SflCtl* __restrict__ c) {
-  sfl::wave::run<PPL, SPL>(*m, *s, *c);
+  sfl::wave::run<PPL, SPL, TW>(*m, *s, *c);
 }
 
 // graph-partitioned rounds (sfl_part.h): local env step (lane per env), segment headers,
@@ -183,9 +183,12 @@ struct HipBackend {
     const auto* ps = (const sfl::SflState*)(base + os);
     const auto* pc = (const sfl::SflCtl*)(base + oc);
     const unsigned wblocks = (unsigned)(((size_t)s.E * 64 + 255) / 256);
-    if (variant == 1) k_wave<sfl::kVariants[1].PPL, sfl::kVariants[1].SPL><<<wblocks, 256, 0, stream>>>(pm, ps, pc);
-    else if (variant == 2) k_wave<sfl::kVariants[2].PPL, sfl::kVariants[2].SPL><<<wblocks, 256, 0, stream>>>(pm, ps, pc);
-    else if (variant == 3) k_wave<sfl::kVariants[3].PPL, sfl::kVariants[3].SPL><<<wblocks, 256, 0, stream>>>(pm, ps, pc);
+#define SFL_KW(v) k_wave<sfl::kVariants[v].PPL, sfl::kVariants[v].SPL, sfl::kVariants[v].TW><<<wblocks, 256, 0, stream>>>(pm, ps, pc)
+    if (variant == 1) SFL_KW(1);
+    else if (variant == 2) SFL_KW(2);
+    else if (variant == 3) SFL_KW(3);
+    else if (variant == 4) SFL_KW(4);
+#undef SFL_KW
     else if (m.T <= 32) k_run<1><<<blocks, 256, 0, stream>>>(pm, ps, pc);
     else if (m.T <= 64) k_run<2><<<blocks, 256, 0, stream>>>(pm, ps, pc);
     else k_run<4><<<blocks, 256, 0, stream>>>(pm, ps, pc);

@@ -79,11 +79,12 @@ struct Handle {
 
 // One-env-per-wavefront kernel shapes (sfl_wave.h): PPL semaphore and SPL counter registers
 // per lane (ports <= 64*PPL, switches <= 64*SPL).  Index 0 = the lane-per-env kernel (k_run).
+// TW: trains per env the variant's LDS prefetch records are sized for (T <= TW).
 struct WaveShape {
-  int PPL, SPL;
+  int PPL, SPL, TW;
 };
-constexpr WaveShape kVariants[] = {{0, 0}, {1, 1}, {4, 1}, {8, 2}};
-constexpr int kNumVariants = 4;
+constexpr WaveShape kVariants[] = {{0, 0, 0}, {1, 1, 32}, {4, 1, 32}, {4, 1, 64}, {8, 2, 64}};
+constexpr int kNumVariants = 5;
 
 // Eligibility: trains fit one lane each (T <= 64, 64-bit masks), the env fits the variant's
 // registers and every semaphore time fits the 11-bit register field.  SFL_KERNEL=scalar
@@ -105,7 +106,7 @@ inline int choose_variant(const sfl_map_desc* md, bool backend_has_wave) {
   if (t_hi > 1023 || ed_min - 2 < -1024) return 0;
   if (md->q_per_env >= (1ull << 32) || (int64_t)md->H * md->W >= (1 << 20) - 1) return 0;
   for (int v = 1; v < kNumVariants; ++v) {
-    if (md->S * 4 <= 64 * kVariants[v].PPL && md->S <= 64 * kVariants[v].SPL) return v;
+    if (md->S * 4 <= 64 * kVariants[v].PPL && md->S <= 64 * kVariants[v].SPL && md->T <= kVariants[v].TW) return v;
   }
   return 0;
 }

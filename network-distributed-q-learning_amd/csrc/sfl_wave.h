@@ -40,7 +40,7 @@ constexpr uint32_t PF_NONE = 0xFFFFFFFFu;
 // from PF_I: distance-map value at the train's cell (observation), at its projected cell if it
 // stops (reward of STOP), and if it moves with final rail action 0..3 (reward of a route)
 constexpr int PF_W = 10, PF_I = 12;
-constexpr int EPS_WIN = 1024;  // epsilon table entries kept in LDS
+constexpr int EPS_WIN = 512;  // epsilon table entries kept in LDS
 constexpr int32_t PF_OFFGRID = (int32_t)0x80000000;  // projection left the grid
 
 #define SFL_AS_G __attribute__((address_space(1)))
@@ -1131,10 +1131,10 @@ struct WEnv {
 };
 
 // driver: one env per wavefront until its episode target / decision budget (env_run in sfl_core.h)
-template <int PPL, int SPL>
+template <int PPL, int SPL, int TW>
 __device__ void run(const SflMap& m, const SflState& s, const SflCtl& c) {
   using V = WEnv<PPL, SPL>;
-  constexpr int LDS_WORDS = 64 * (PPL + SPL) + 64 * PF_W * 2;  // semaphores, counters, prefetch
+  constexpr int LDS_WORDS = 64 * (PPL + SPL) + TW * PF_W * 2;  // semaphores, counters, prefetch records
   const int lane = (int)__lane_id();
   const uint32_t e = uni((uint32_t)((blockIdx.x * blockDim.x + threadIdx.x) >> 6));
   __shared__ double leps[EPS_WIN];
