@@ -17,7 +17,7 @@
 #include "sfl_wave.h"
 
 #ifndef SFL_WAVE_OCC
-#define SFL_WAVE_OCC 4  // waves per SIMD the one-env-per-wave kernel is register-budgeted for
+#define SFL_WAVE_OCC 5  // waves per SIMD the one-env-per-wave kernel is register-budgeted for (5: 96 VGPRs)
 #endif
 
 namespace {
@@ -34,10 +34,10 @@ __global__ void __launch_bounds__(256) k_run(const sfl::SflMap* __restrict__ m, 
 
 // One env per wavefront (sfl_wave.h): 4 envs per block.  PPL / SPL = semaphore / counter
 // registers per lane (sfl::kVariants).
-template <int PPL, int SPL, int TW>
+template <int PPL, int SPL, int TW, bool TRACE>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SFL_WAVE_OCC))) k_wave(const sfl::SflMap* __restrict__ m, const sfl::SflState* __restrict__ s,
                                               const sfl::SflCtl* __restrict__ c) {
-  sfl::wave::run<PPL, SPL, TW>(*m, *s, *c);
+  sfl::wave::run<PPL, SPL, TW, TRACE>(*m, *s, *c);
 }
 
 // graph-partitioned rounds (sfl_part.h): local env step (lane per env), segment headers,
@@ -183,7 +183,9 @@ struct HipBackend {
     const auto* ps = (const sfl::SflState*)(base + os);
     const auto* pc = (const sfl::SflCtl*)(base + oc);
     const unsigned wblocks = (unsigned)(((size_t)s.E * 64 + 255) / 256);
-#define SFL_KW(v) k_wave<sfl::kVariants[v].PPL, sfl::kVariants[v].SPL, sfl::kVariants[v].TW><<<wblocks, 256, 0, stream>>>(pm, ps, pc)
+#define SFL_KW(v)                                                                                                   \
+  (c.trace ? k_wave<sfl::kVariants[v].PPL, sfl::kVariants[v].SPL, sfl::kVariants[v].TW, true><<<wblocks, 256, 0, stream>>>(pm, ps, pc) \
+           : k_wave<sfl::kVariants[v].PPL, sfl::kVariants[v].SPL, sfl::kVariants[v].TW, false><<<wblocks, 256, 0, stream>>>(pm, ps, pc))
     if (variant == 1) SFL_KW(1);
     else if (variant == 2) SFL_KW(2);
     else if (variant == 3) SFL_KW(3);

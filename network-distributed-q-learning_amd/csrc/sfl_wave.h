@@ -147,7 +147,7 @@ struct PortRec {
   __device__ __forceinline__ uint32_t q_off() const { return w[3]; }
 };
 // PPL semaphore registers (ports <= 64*PPL) and SPL counter registers (switches <= 64*SPL) per lane
-template <int PPL, int SPL>
+template <int PPL, int SPL, int TWc>
 struct WEnv {
   const SflMap& m;
   const SflState& s;
@@ -185,8 +185,10 @@ struct WEnv {
   int32_t now;
   uint32_t flags, epoch;
   uint64_t q_mask, arr_mask, fl_mask, mf_mask;
-  Pcg64 rng;
-  double cum;
+  // the epsilon-greedy stream (numpy PCG64 state, increment, buffered half) lives in LDS: it is
+  // touched once per decision and would otherwise hold ten registers across the whole loop
+  uint64_t* lrng;  // [6]: state hi, lo, inc hi, lo, has << 32 | buf
+  int64_t cum;     // cumulative reward: a sum of integer rewards, exact in f64 (converted on store)
   int32_t n_mf, ep_dec, ep_ticks;
   int32_t step_ctr;
   uint32_t n_dec;  // decisions in this launch (dec_total += n_dec on store)
@@ -196,6 +198,7 @@ struct WEnv {
 
   __device__ WEnv(const SflMap& m_, const SflState& s_, uint32_t e_, int lane_, uint32_t* lds, const double* leps_)
       : m(m_), s(s_), e(e_), E(s_.E), lane(lane_), mine(lane_ < m_.T), lsem(lds), lcnt(lds + 64 * PPL), lpf((double*)(lds + 64 * (PPL + SPL))), leps(leps_) {
+    lrng = (uint64_t*)(lds + 64 * (PPL + SPL) + TWc * PF_W * 2);
     qb = s.q + (size_t)e * m.q_per_env;
     pf_ok = false;
     pf_roff = pf_qoff = PF_NONE;
@@ -412,14 +415,8 @@ struct WEnv {
     arr_mask = mask(1);
     fl_mask = mask(2);
     mf_mask = mask(3);
-    rng.shi = uni(ld(s.rng, ix(0)));
-    rng.slo = uni(ld(s.rng, ix(1)));
-    rng.ihi = uni(ld(s.rng, ix(2)));
-    rng.ilo = uni(ld(s.rng, ix(3)));
-    const uint64_t hb = uni(ld(s.rng, ix(4)));
-    rng.has = (uint32_t)(hb >> 32);
-    rng.buf = (uint32_t)hb;
-    cum = unid(ld(s.cum_reward, e));
+    if (lane < 5) lrng[lane] = ld(s.rng, ix((size_t)lane));
+    cum = (int64_t)unid(ld(s.cum_reward, e));
     n_mf = uni(ld(s.n_mf, e));
     ep_dec = uni(ld(s.ep_dec, e));
     ep_ticks = uni(ld(s.ep_ticks, e));
@@ -465,10 +462,10 @@ struct WEnv {
       st(s.masks, (size_t)(2 * MAXW + 1) * E + e, (uint32_t)(fl_mask >> 32));
       st(s.masks, (size_t)(3 * MAXW + 0) * E + e, (uint32_t)mf_mask);
       st(s.masks, (size_t)(3 * MAXW + 1) * E + e, (uint32_t)(mf_mask >> 32));
-      st(s.rng, ix(0), rng.shi);
-      st(s.rng, ix(1), rng.slo);
-      st(s.rng, ix(4), ((uint64_t)rng.has << 32) | rng.buf);
-      st(s.cum_reward, e, cum);
+      st(s.rng, ix(0), lrng[0]);
+      st(s.rng, ix(1), lrng[1]);
+      st(s.rng, ix(4), lrng[4]);
+      st(s.cum_reward, e, (double)cum);
       st(s.n_mf, e, n_mf);
       st(s.ep_dec, e, ep_dec);
       st(s.ep_ticks, e, ep_ticks);
@@ -501,7 +498,7 @@ struct WEnv {
       for (int i = lane; i < m.S * m.T; i += 64) st(slotb, (size_t)i, slot_make(PEND_NONE, 0, 0));
       epoch = 1;
     }
-    cum = 0.0;
+    cum = 0;
     n_mf = 0;
     ep_dec = 0;
     ep_ticks = 0;
@@ -916,6 +913,16 @@ struct WEnv {
     int action = -1;
     bool explore = false;
     if (!greedy) {
+      // (kept in VGPRs: the 128-bit LCG runs on the vector ALU's 64-bit multiply-adds; the scalar
+      // unit is the contended one)
+      Pcg64 rng;
+      rng.shi = lrng[0];
+      rng.slo = lrng[1];
+      rng.ihi = lrng[2];
+      rng.ilo = lrng[3];
+      const uint64_t hb = lrng[4];
+      rng.has = (uint32_t)(hb >> 32);
+      rng.buf = (uint32_t)hb;
       const uint32_t n = cget(sw);
       const double eps = n < (uint32_t)EPS_WIN && n < (uint32_t)m.ntab ? unid(leps[n])
                          : n < (uint32_t)m.ntab                      ? ldc(m.eps_tab, (size_t)n)
@@ -930,6 +937,11 @@ struct WEnv {
         uint32_t mk = amask;
         for (uint32_t kk = 0; kk < pick; ++kk) mk &= mk - 1u;
         action = __builtin_ctz(mk);
+      }
+      if (lane == 0) {
+        lrng[0] = rng.shi;
+        lrng[1] = rng.slo;
+        lrng[4] = ((uint64_t)rng.has << 32) | rng.buf;
       }
     }
     d.q_pend = unid(q_pend_v);
@@ -1131,10 +1143,12 @@ struct WEnv {
 };
 
 // driver: one env per wavefront until its episode target / decision budget (env_run in sfl_core.h)
-template <int PPL, int SPL, int TW>
+// TRACE: the per-decision trace of one env (parity tests only) is compiled into a separate
+// instantiation, so the production kernel does not carry its registers
+template <int PPL, int SPL, int TW, bool TRACE>
 __device__ void run(const SflMap& m, const SflState& s, const SflCtl& c) {
-  using V = WEnv<PPL, SPL>;
-  constexpr int LDS_WORDS = 64 * (PPL + SPL) + TW * PF_W * 2;  // semaphores, counters, prefetch records
+  using V = WEnv<PPL, SPL, TW>;
+  constexpr int LDS_WORDS = 64 * (PPL + SPL) + TW * PF_W * 2 + 12;  // semaphores, counters, prefetch records, rng
   const int lane = (int)__lane_id();
   const uint32_t e = uni((uint32_t)((blockIdx.x * blockDim.x + threadIdx.x) >> 6));
   __shared__ double leps[EPS_WIN];
@@ -1199,7 +1213,7 @@ __device__ void run(const SflMap& m, const SflState& s, const SflCtl& c) {
         SFL_PT(t0);
         v.post(d, greedy);
         SFL_PACC(3, t0);
-        if (c.trace && (int32_t)e == c.trace_env) {
+        if (TRACE && c.trace && (int32_t)e == c.trace_env) {
           const uint64_t cs = v.sem_checksum();
           if (lane == 0) {
             const uint64_t n = *c.trace_n;
@@ -1215,7 +1229,7 @@ __device__ void run(const SflMap& m, const SflState& s, const SflCtl& c) {
           }
         }
         v.flags &= ~F_INFLIGHT;
-        v.cum += (double)d.reward;
+        v.cum += d.reward;
         v.ep_dec += 1;
         v.n_dec += 1;
         v.step_ctr += 1;
@@ -1231,7 +1245,7 @@ __device__ void run(const SflMap& m, const SflState& s, const SflCtl& c) {
         const int32_t idx = (greedy && test_mode) ? n_test : ep_t;
         const size_t row = (size_t)(idx - c.stats_base) % cap;
         if (lane == 0) {
-          st(c.st_cum, row * s.E + e, v.cum);
+          st(c.st_cum, row * s.E + e, (double)v.cum);
           st(c.st_arrived, row * s.E + e, (int32_t)arrived);
           st(c.st_mf, row * s.E + e, v.n_mf);
           st(c.st_dec, row * s.E + e, v.ep_dec);
@@ -1241,7 +1255,7 @@ __device__ void run(const SflMap& m, const SflState& s, const SflCtl& c) {
       }
       if (greedy && !test_mode && c.sx_cum && c.stats_cap > 0 && lane == 0) {
         const size_t row = (size_t)(ep_t - c.stats_base) % cap;
-        st(c.sx_cum, row * s.E + e, v.cum);
+        st(c.sx_cum, row * s.E + e, (double)v.cum);
         st(c.sx_arrived, row * s.E + e, (int32_t)arrived);
       }
       if (greedy) {
