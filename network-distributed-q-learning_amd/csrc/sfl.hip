@@ -202,14 +202,17 @@ struct HipBackend {
     *ms = t;
 #ifdef SFL_PROFILE
     if (variant > 0) {
-      unsigned long long pr[16] = {};
+      unsigned long long pr[32] = {};
       hipMemcpyFromSymbol(pr, HIP_SYMBOL(sfl::wave::g_prof), sizeof pr);
       fprintf(stderr,
               "[sfl profile] cycles reset %.3e tick %.3e decide %.3e (observe %.3e egreedy %.3e apply %.3e) post %.3e "
               "total %.3e | prefetch %llu row hit %llu miss %llu pend hit %llu miss %llu decisions %llu\n",
               (double)pr[0], (double)pr[1], (double)pr[2], (double)pr[5], (double)pr[6], (double)pr[7], (double)pr[3],
               (double)pr[4], pr[8], pr[9], pr[10], pr[11], pr[12], pr[13]);
-      unsigned long long z[16] = {};
+      fprintf(stderr, "[sfl laps]");
+      for (int k = 0; k < 16; ++k) fprintf(stderr, " %d:%.3e", k, (double)pr[16 + k]);
+      fprintf(stderr, "\n");
+      unsigned long long z[32] = {};
       hipMemcpyToSymbol(HIP_SYMBOL(sfl::wave::g_prof), z, sizeof z);
     }
 #endif

@@ -231,6 +231,15 @@ int create(const sfl_map_desc* md, const sfl_hparams* hp, uint32_t n_envs, const
       pp[p * 4 + 2] = md->row_base[p];
       pp[p * 4 + 3] = (uint32_t)md->q_off[p];
     }
+    std::vector<uint32_t> ptr_(NP * 4, 0);
+    for (size_t o = 0; o < NP; ++o) {
+      const int t = md->port_nb[o];
+      const int u = t >= 0 ? md->port_unique[t] : -1;
+      const int far = u >= 0 ? md->port_nb[u] : -1;
+      ptr_[o * 4 + 0] = (uint32_t)(uint16_t)(int16_t)t | ((uint32_t)(uint16_t)(int16_t)u << 16);
+      ptr_[o * 4 + 1] = (uint32_t)(uint16_t)(int16_t)far | ((uint32_t)(uint16_t)md->port_len[o] << 16);
+      ptr_[o * 4 + 2] = u >= 0 ? (uint32_t)(uint16_t)md->port_len[u] : 0u;
+    }
     for (size_t c = 0; c < HW; ++c)
       for (int d = 0; d < 4; ++d)
         for (int a = 0; a < 4; ++a)
@@ -256,6 +265,8 @@ int create(const sfl_map_desc* md, const sfl_hparams* hp, uint32_t n_envs, const
     m.port_pack = h->upload(h->keep.back().data(), h->keep.back().size());
     h->keep.push_back(std::move(mv));
     m.move_tab = h->upload(h->keep.back().data(), h->keep.back().size());
+    h->keep.push_back(std::move(ptr_));
+    m.port_tr = h->upload(h->keep.back().data(), h->keep.back().size());
     h->keep.emplace_back(trp.begin(), trp.end());
     m.tr_pack = (const int32_t*)h->upload(h->keep.back().data(), h->keep.back().size());
   }

@@ -25,21 +25,31 @@ namespace wave {
 #ifdef SFL_PROFILE
 // tuning builds only: wall cycles per phase summed over waves (reset, tick, decide, post, total,
 // decide = observe + egreedy + apply)
-__device__ unsigned long long g_prof[16];
+__device__ unsigned long long g_prof[32];
 #define SFL_PCNT(k) (prof[k] += 1)
+#define SFL_LAP0() (lap_t = (uint64_t)__builtin_amdgcn_s_memtime())
+#define SFL_LAP(k)                                                 \
+  do {                                                             \
+    const uint64_t _t = (uint64_t)__builtin_amdgcn_s_memtime();   \
+    lap[k] += _t - lap_t;                                          \
+    lap_t = _t;                                                    \
+  } while (0)
 #define SFL_PT(var) const uint64_t var = (uint64_t)__builtin_amdgcn_s_memtime()
 #define SFL_PACC(k, t0) prof[k] += (uint64_t)__builtin_amdgcn_s_memtime() - (t0)
 #else
 #define SFL_PT(var)
 #define SFL_PACC(k, t0)
 #define SFL_PCNT(k)
+#define SFL_LAP0()
+#define SFL_LAP(k)
 #endif
 
 constexpr uint32_t PF_NONE = 0xFFFFFFFFu;
-// batch-prefetch record per train (doubles): row 0-3, pending cell 4, slot word 5, then int32 words
-// from PF_I: distance-map value at the train's cell (observation), at its projected cell if it
-// stops (reward of STOP), and if it moves with final rail action 0..3 (reward of a route)
-constexpr int PF_W = 10, PF_I = 12;
+// batch-prefetch record per train (doubles): row 0-3, pending cell 4, slot word 5, the row's max 6,
+// then int32 words from PF_I: distance-map value at the train's cell (observation), at its
+// projected cell if it stops (reward of STOP), if it moves with final rail action 0..3 (reward of
+// a route), and the row's argmax | first allowed argmax << 8 under the staged observation
+constexpr int PF_W = 12, PF_I = 14;
 constexpr int EPS_WIN = 512;  // epsilon table entries kept in LDS
 constexpr int32_t PF_OFFGRID = (int32_t)0x80000000;  // projection left the grid
 
@@ -194,6 +204,8 @@ struct WEnv {
   uint32_t n_dec;  // decisions in this launch (dec_total += n_dec on store)
 #ifdef SFL_PROFILE
   uint64_t prof[9] = {};  // decide: observe, epsilon-greedy, apply; events: prefetch, row hit/miss, pend hit/miss, decisions
+  uint64_t lap[16] = {};  // finer segments (see SFL_LAP call sites)
+  uint64_t lap_t = 0;
 #endif
 
   __device__ WEnv(const SflMap& m_, const SflState& s_, uint32_t e_, int lane_, uint32_t* lds, const double* leps_)
@@ -278,8 +290,8 @@ struct WEnv {
     }
   }
   __device__ __forceinline__ int32_t dist_v(int k, int cell, int dir) const {
-    if (cell < 0) return PF_OFFGRID;
-    return ld(m.dist, ((uint32_t)k * (uint32_t)m.HW + (uint32_t)cell) * 4u + (uint32_t)dir);
+    const int32_t d = ld(m.dist, ((uint32_t)k * (uint32_t)m.HW + (uint32_t)(cell >= 0 ? cell : 0)) * 4u + (uint32_t)dir);
+    return cell < 0 ? PF_OFFGRID : d;
   }
   // distance staged by prefetch (dist() semantics: off the grid or unreachable sets E_INF_DIST)
   __device__ __forceinline__ int32_t dist_staged(int32_t d) {
@@ -345,6 +357,55 @@ struct WEnv {
     }
     return bl;
   }
+  // put_keep / put_replace as value transforms of a record (vector ALU, wave-uniform values)
+  struct PutF {
+    uint32_t h, in;
+    int32_t now, span, ovr;  // ovr: in-flag that is overridden (-1: none)
+    bool keep;               // put_keep: an overridden record keeps its in-flag
+    __device__ __forceinline__ uint32_t operator()(uint32_t r) const {
+      const uint32_t nr = r_pack(h, keep ? r_in(r) : in, now, now + span);
+      const uint32_t fresh = r_pack(h, in, now, now + span);
+      if (!r_present(r)) return fresh;
+      if ((ovr >= 0 && r_in(r) == (uint32_t)ovr) || r_t0(r) > now) return nr;
+      return r;
+    }
+  };
+  __device__ __forceinline__ PutF put_keep_f(int h, uint32_t in, int32_t span, uint32_t ovr_in) const {
+    return PutF{(uint32_t)h, in, now, span, (int32_t)ovr_in, true};
+  }
+  __device__ __forceinline__ PutF put_replace_f(int h, uint32_t in, int32_t span, int ovr_in) const {
+    return PutF{(uint32_t)h, in, now, span, ovr_in, false};
+  }
+  // register copies of the records of up to four ports (index -1 = unused)
+  struct SemQuad {
+    uint32_t* l;
+    int p[4];
+    uint32_t v[4];
+    __device__ __forceinline__ SemQuad(uint32_t* l_, int a, int b, int c, int d) : l(l_) {
+      p[0] = a;
+      p[1] = b;
+      p[2] = c;
+      p[3] = d;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = l[p[i] >= 0 ? p[i] : 0];
+    }
+    template <class F>
+    __device__ __forceinline__ void put(int port, const F& f) {
+      uint32_t cur = v[0];
+#pragma unroll
+      for (int i = 3; i > 0; --i) cur = (p[i] == port) ? v[i] : cur;
+      const uint32_t nv = f(cur);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = (p[i] == port) ? nv : v[i];
+    }
+    __device__ __forceinline__ void store(int lane) const {
+      if (lane == 0) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (p[i] >= 0) l[p[i]] = v[i];
+      }
+    }
+  };
   // set if absent, else (io == ovr_io or t0 in the future) -> retime in place (io kept)
   __device__ __forceinline__ void put_keep(int p, int h, uint32_t in, int32_t span, uint32_t ovr_in) {
     const uint32_t r = sget(p);
@@ -508,6 +569,7 @@ struct WEnv {
   // ---- one Flatland tick + switchfl bookkeeping (switch_env.py:296-401, 427-485;
   //      flatland_lite.RailEnv.step), train-parallel: lane h = train h ----------------------------
   __device__ __forceinline__ void tick() {
+    SFL_LAP0();
     pf_ok = false;
     const int32_t t = ++now;
     const uint64_t seed = s.seed[e];
@@ -574,6 +636,7 @@ struct WEnv {
       aux |= pa | (ddir << 4) | (given << 8);
       bits = tb_make(dir, st_, prev, saved, mf, tb_done(b));
     }
+    SFL_LAP(11);
     // pass 2: motion check, least fixed point (flatland_lite.motion_check): the lowest handle
     // wanting a cell wins it; a cell can be entered if free or its occupant moves out
     const uint64_t M = __ballot(mover);
@@ -600,6 +663,7 @@ struct WEnv {
         A |= nb;
       }
     }
+    SFL_LAP(12);
     // pass 3: state machine + positions, deviation fix
     const bool over = t >= m.max_episode_steps;
     bool done = false, isdone = !mine, newly = false, dep = false;
@@ -660,6 +724,7 @@ struct WEnv {
       bits = tb_make(dir, st_, tb_prev(b), saved, mf, done ? 1u : 0u);
     }
     arr_mask |= __ballot(newly);
+    SFL_LAP(13);
     // delete the semaphores of done trains (switch_env.py:370-376): each lane its own records
     const uint64_t DONE = __ballot(done);
     if (DONE) {
@@ -696,6 +761,7 @@ struct WEnv {
     const uint64_t MF = __ballot(mine && tb_mf(bits) > 0);
     n_mf += popc64(MF & ~mf_mask);
     mf_mask = MF;
+    SFL_LAP(14);
     // _check_active_switch (switch_env.py:427-485)
     bool act = false;
     if (mine && pos >= 0 && st4 != S_WAITING) {
@@ -718,6 +784,7 @@ struct WEnv {
       }
     }
     q_mask = __ballot(act);
+    SFL_LAP(15);
     const uint64_t full = (m.T == 64) ? ~0ull : ((1ull << m.T) - 1ull);
     const uint64_t ALL = __ballot(isdone);
     ep_ticks += 1;
@@ -736,16 +803,53 @@ struct WEnv {
     const uint64_t malf = __ballot(mine && tb_state(bits) == S_MALF);
     pf_roff = pf_qoff = PF_NONE;
     if (!((q_mask >> lane) & 1ull)) return;
+    // Loads are issued by dependency level, unconditionally (clamped indices), so the chains
+    // overlap: level 1 needs only this lane's registers, level 2 the level-1 results, ...
     const int sw = (int)(sdec >> 16);
+    const int pin = (int)(nprv & 0xFFFFu);
+    const int slot = pin & 3;
+    const int dir0 = (int)tb_dir(bits);
+    const int pos0 = pos >= 0 ? pos : 0;
     double* pfl = lpf + PF_W * lane;
+    int32_t* pfi = (int32_t*)pfl + PF_I;
+    // level 1: slot word, switch record, timetable row, the row block's port record, first moves
     const uint64_t slw = ld(slotb, slot_ix(sw, lane));
     const u4 w0 = ld((const u4*)m.sw_pack, (size_t)sw * 4u);
+    const u4 w4 = ld((const u4*)m.sw_pack, (size_t)sw * 4u + 1u);  // compact-row descriptors
     const vec_t<uint32_t, 2> nbw = ld((const vec_t<uint32_t, 2>*)m.sw_pack, (size_t)sw * 8u + 4u);
-    const int32_t la = ld(m.tr_pack, (size_t)lane * 8 + 1), k = ld(m.tr_pack, (size_t)lane * 8 + 2);
+    const u4 trw = ld((const u4*)m.tr_pack, (size_t)lane * 2u);  // ed, la, k, target
+    const u4 pr = ld((const u4*)m.port_pack, (size_t)(4 * sw + slot));
+    const uint32_t n_plan = pl_len(plan);
+    const uint32_t a1 = n_plan ? pl_front(plan) : A_FWD;
+    const Move m1 = check_action<false>(a1, pos0, dir0);  // projection of a route: first rail action
+    // distances the decision needs (reward_func.py:23-78): at the cell, along the STOP plan
+    // ([STOP] + plan) and along each route's plan ([front or FWD, final rail action 0..3])
+    const int32_t la = (int32_t)trw[1], k = (int32_t)trw[2];
+    const int32_t dd = dist_v(k, pos, dir0);
+    {
+      int pc = pos, pd = dir0;
+      for (uint32_t i = 0; i < n_plan; ++i) project(pl_at(plan, i), pc, pd);
+      pfi[1] = dist_v(k, pc, pd);
+    }
+    {
+      int pc = pos, pd = dir0;
+      if (a1 != A_STOP && pos >= 0) {
+        pc = m1.cell;
+        pd = m1.dir;
+      }
+#pragma unroll
+      for (uint32_t t = 0; t < 4; ++t) {
+        int qc = pc, qd = pd;
+        project(t, qc, qd);
+        pfi[2 + t] = dist_v(k, qc, qd);
+      }
+    }
+    pfi[0] = dd;
+    // level 2: the pending update's block; the observation (LDS) and its row
+    const uint32_t pend = greedy ? PEND_NONE : slot_pend(slw, epoch);
+    const bool hp = pend != PEND_NONE;
+    const u4 pp = ld((const u4*)m.port_pack, (size_t)(hp ? 4 * (pend & 0xFFFu) + ((pend >> 12) & 3u) : 0u));
     const int np = (int)(w0[0] & 15u);
-    const int pin = (int)(nprv & 0xFFFFu);
-    int slot = pin & 3;
-    if ((pin >> 2) != sw || slot >= np) slot = 0;
     uint32_t fb = 0;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -754,49 +858,55 @@ struct WEnv {
       const uint32_t blk = rec_blocks(lsem[nb], (uint32_t)lane, malf, 0u) | rec_blocks(lsem[p], (uint32_t)lane, malf, 1u);
       fb |= (blk == 0u && j < np) ? (1u << j) : 0u;
     }
-    // distances the decision needs (reward_func.py:23-78): at the cell, and at the projection of
-    // the plan the decision leaves (STOP: [STOP] + plan; a route: [front or FWD, final action])
-    int32_t* pfi = (int32_t*)pfl + PF_I;
-    const int dir0 = (int)tb_dir(bits);
-    const int32_t dd = dist_v(k, pos, dir0);
-    pfi[0] = dd;
-    {
-      int pc = pos, pd = dir0;
-      const uint32_t n = pl_len(plan);
-      for (uint32_t i = 0; i < n; ++i) project(pl_at(plan, i), pc, pd);
-      pfi[1] = dist_v(k, pc, pd);
-    }
-    {
-      int pc = pos, pd = dir0;
-      project(pl_len(plan) ? pl_front(plan) : A_FWD, pc, pd);
+    const int32_t dl = now - la + dd;
+    const int32_t avail = la - (int32_t)trw[0];
+    const uint32_t lvl = dl <= 0 ? 0u : (dl <= avail * 20 ? 1u : 2u);
+    const uint32_t state = ((fb * (uint32_t)m.K) + (uint32_t)k) * 3u + lvl;
+    const uint32_t w = pr[1] >> 16, roff = pr[3] + state * w;
+    const bool row_ok = pos >= 0 && dd < DIST_INF && (pin >> 2) == sw && slot < np;
+    const uint32_t qoff = pp[3] + ((pend >> 14) & 0x3FFFu) * (pp[1] >> 16) + ((pend >> 28) & 3u);
+    // level 3: Q values
+    const double* rp = qbase() + (row_ok ? roff : 0u);
+    double rv[4];
 #pragma unroll
-      for (uint32_t t = 0; t < 4; ++t) {
-        int qc = pc, qd = pd;
-        project(t, qc, qd);
-        pfi[2 + t] = dist_v(k, qc, qd);
+    for (int c = 0; c < 4; ++c) rv[c] = ld(rp, (size_t)((uint32_t)c < w ? c : 0));
+    const double qv = ld(qbase(), (size_t)(hp ? qoff : 0u));
+#pragma unroll
+    for (int c = 0; c < 4; ++c) pfl[c] = rv[c];
+    // the greedy choice on the staged row (distr_q.py:449-490, as in decide): valid whenever the
+    // row is (a decision uses it only if its observation is the staged one)
+    {
+      const uint32_t rd = w4[slot];
+      const int na = (int)((w0[0] >> 4) & 15u);
+      uint32_t am = 1u << (na - 1);
+      for (int a = 0; a < na - 1; ++a)
+        if ((int)((w0[1] >> (2 * a)) & 3u) == slot && ((fb >> ((w0[1] >> (16 + 2 * a)) & 3u)) & 1u)) am |= 1u << a;
+      const int mind = (int)((rd >> 16) & 15u);
+      double mx = mind != 15 ? m.default_q : -__builtin_huge_val();
+      int best = mind != 15 ? mind : 99, arg = -1;
+      double amx = 0.0;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        if ((uint32_t)c < w) {
+          const int a = (int)((rd >> (4 * c)) & 15u);
+          const double v = rv[c];
+          if (v > mx || (v == mx && a < best)) {
+            mx = v;
+            best = a;
+          }
+          if (((am >> a) & 1u) && (arg < 0 || v > amx || (v == amx && a < arg))) {
+            arg = a;
+            amx = v;
+          }
+        }
       }
+      pfl[6] = mx;
+      pfi[6] = (best & 0xFF) | ((arg & 0xFF) << 8);
     }
-    if (pos >= 0 && dd < DIST_INF) {
-      const int32_t dl = now - la + dd;
-      const int32_t avail = la - t_ed;
-      const uint32_t lvl = dl <= 0 ? 0u : (dl <= avail * 20 ? 1u : 2u);
-      const uint32_t state = ((fb * (uint32_t)m.K) + (uint32_t)k) * 3u + lvl;
-      const u4 pr = ld((const u4*)m.port_pack, (size_t)(4 * sw + slot));
-      const uint32_t w = pr[1] >> 16, roff = pr[3] + state * w;
-      const double* rp = qbase() + roff;
-#pragma unroll
-      for (int c = 0; c < 4; ++c)
-        if ((uint32_t)c < w) pfl[c] = ld(rp, (size_t)c);
-      pf_roff = roff;
-    }
-    const uint32_t pend = greedy ? PEND_NONE : slot_pend(slw, epoch);
-    if (pend != PEND_NONE) {
-      const u4 pr = ld((const u4*)m.port_pack, (size_t)(4 * (pend & 0xFFFu) + ((pend >> 12) & 3u)));
-      const uint32_t qoff = pr[3] + ((pend >> 14) & 0x3FFFu) * (pr[1] >> 16) + ((pend >> 28) & 3u);
-      pfl[4] = ld(qbase(), (size_t)qoff);
-      pf_qoff = qoff;
-    }
+    pfl[4] = qv;
     pfl[5] = __longlong_as_double((long long)slw);
+    pf_roff = row_ok ? roff : PF_NONE;
+    pf_qoff = hp ? qoff : PF_NONE;
   }
   // a Q cell of this env was written (uniform offset): drop staged copies that contain it
   __device__ __forceinline__ void pf_written(uint32_t off) {
@@ -821,12 +931,14 @@ struct WEnv {
 
   __device__ __forceinline__ void decide(Dec& d, bool greedy) {
     SFL_PT(t_obs);
+    SFL_LAP0();
     // agent_iter: lowest queued train (switch_env.py:418-421, 616-622)
     if (!pf_ok) {
       prefetch(greedy);
       pf_ok = true;
       SFL_PCNT(3);
     }
+    SFL_LAP(0);
     SFL_PCNT(8);
     const int h = ctz64(q_mask);
     q_mask &= q_mask - 1ull;
@@ -835,7 +947,20 @@ struct WEnv {
     const SwRec swr = sw_rec(sw);
     const vec_t<int32_t, 8> tr = ldcv<vec_t<int32_t, 8>>(m.tr_pack, (size_t)h);
     const double* pfh = lpf + PF_W * h;
-    const uint64_t slot_v = (uint64_t)__double_as_longlong(pfh[5]);  // staged by prefetch (never stale)
+    // the decision's LDS reads that do not depend on its observation, issued together: the staged
+    // slot word (never stale: a decision writes only its own train's slots), row column, pending
+    // cell value and distances, the epsilon-greedy stream and the switch's interaction count
+    const uint64_t slot_v = (uint64_t)__double_as_longlong(pfh[5]);
+    const double pf_qp = pfh[4];
+    const double pf_mx = pfh[6];
+    const vec_t<int32_t, 2> pfd01 = *(const vec_t<int32_t, 2>*)((const int32_t*)pfh + PF_I);
+    const vec_t<int32_t, 2> pfd23 = *(const vec_t<int32_t, 2>*)((const int32_t*)pfh + PF_I + 2);
+    const vec_t<int32_t, 2> pfd45 = *(const vec_t<int32_t, 2>*)((const int32_t*)pfh + PF_I + 4);
+    const vec_t<int32_t, 2> pfd67 = *(const vec_t<int32_t, 2>*)((const int32_t*)pfh + PF_I + 6);
+    uint64_t rng_w[5];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) rng_w[i] = lrng[i];
+    const uint32_t n_sw = cget(sw);
     const uint32_t pf_roff_h = rl(pf_roff, h), pf_qoff_h = rl(pf_qoff, h);
     const int np = swr.np();
     const int na = swr.na();
@@ -847,6 +972,7 @@ struct WEnv {
       lerr |= E_PORT;
       slot = 0;
     }
+    SFL_LAP(1);
     // observe: lane j < np evaluates check_port_blocked(next_port(p_j), p_j) for port j of the
     // switch (observer.py:44-151, 269-283), branch-free integer VALU, then one ballot; lane a
     // evaluates get_action_mask for route a (switch_agents.py:104-134)
@@ -859,11 +985,11 @@ struct WEnv {
     const uint32_t rn = lsem[nbj], ro = lsem[pj];
     const uint32_t blk = rec_blocks(rn, (uint32_t)h, malf, 0u) | rec_blocks(ro, (uint32_t)h, malf, 1u);
     const uint32_t free_bits = (uint32_t)__ballot(pvalid && blk == 0u) & 15u;
+    SFL_LAP(2);
     const uint32_t b = rl(bits, h);
     const int32_t p0 = rl(pos, h);
     const int32_t ed = tr[0], la = tr[1], k = tr[2];
-    const int32_t* pfih = (const int32_t*)pfh + PF_I;
-    const int32_t dl = now - la + dist_staged(uni(pfih[0]));
+    const int32_t dl = now - la + dist_staged(uni(pfd01[0]));
     const int32_t avail = la - ed;
     const uint32_t lvl = dl <= 0 ? 0u : (dl <= avail * 20 ? 1u : 2u);
     const uint32_t state = ((free_bits * (uint32_t)m.K) + (uint32_t)k) * 3u + lvl;
@@ -872,6 +998,7 @@ struct WEnv {
     const uint32_t amask =
         ((uint32_t)__ballot(lane < na - 1 && srca == (uint32_t)slot && ((free_bits >> dsta) & 1u)) & 0xFFu) |
         (1u << (na - 1));
+    SFL_LAP(3);
     SFL_PACC(0, t_obs);
     SFL_PT(t_eg);
     // issue the Q row load and the pending update's Q cell load, then draw while they fly
@@ -880,14 +1007,15 @@ struct WEnv {
     const uint32_t roff = prr.q_off() + state * (uint32_t)w;
     // lane c < w holds compact column c of the row (staged by prefetch unless stale)
     const bool colv = lane < w;
-    double v_c;
-    if (pf_roff_h == roff) {
-      v_c = pfh[lane & 3];
+    const bool row_hit = pf_roff_h == roff;  // the staged row and its greedy choice are valid
+    double v_c = 0.0;
+    if (row_hit) {
       SFL_PCNT(4);
     } else {
       v_c = ld(qbase() + roff, (size_t)(colv ? lane : 0));
       SFL_PCNT(5);
     }
+    SFL_LAP(4);
     d.slotword = uni(slot_v);
     const uint32_t pend = greedy ? PEND_NONE : slot_pend(d.slotword, epoch);
     d.qoff_pend = PF_NONE;
@@ -901,7 +1029,7 @@ struct WEnv {
       d.qoff_pend = pr.q_off() + pstate * (uint32_t)pr.q_w() + (uint32_t)pj;
       d.row_pend = pr.row_base() + pstate;
       if (pf_qoff_h == d.qoff_pend) {
-        q_pend_v = pfh[4];
+        q_pend_v = pf_qp;
         SFL_PCNT(6);
       } else {
         q_pend_v = ld(qbase(), (size_t)d.qoff_pend);
@@ -909,6 +1037,7 @@ struct WEnv {
       }
     }
     const int32_t reward = slot_rew(d.slotword, epoch);
+    SFL_LAP(5);
     // epsilon-greedy
     int action = -1;
     bool explore = false;
@@ -916,14 +1045,14 @@ struct WEnv {
       // (kept in VGPRs: the 128-bit LCG runs on the vector ALU's 64-bit multiply-adds; the scalar
       // unit is the contended one)
       Pcg64 rng;
-      rng.shi = lrng[0];
-      rng.slo = lrng[1];
-      rng.ihi = lrng[2];
-      rng.ilo = lrng[3];
-      const uint64_t hb = lrng[4];
+      rng.shi = rng_w[0];
+      rng.slo = rng_w[1];
+      rng.ihi = rng_w[2];
+      rng.ilo = rng_w[3];
+      const uint64_t hb = rng_w[4];
       rng.has = (uint32_t)(hb >> 32);
       rng.buf = (uint32_t)hb;
-      const uint32_t n = cget(sw);
+      const uint32_t n = n_sw;
       const double eps = n < (uint32_t)EPS_WIN && n < (uint32_t)m.ntab ? unid(leps[n])
                          : n < (uint32_t)m.ntab                      ? ldc(m.eps_tab, (size_t)n)
                                                                      : m.eps0 * pow_ool(m.eps_decay, (double)n);
@@ -944,35 +1073,46 @@ struct WEnv {
         lrng[4] = ((uint64_t)rng.has << 32) | rng.buf;
       }
     }
+    SFL_LAP(6);
     d.q_pend = unid(q_pend_v);
     // np.argmax over the full row (first maximum), max(row), and the first allowed maximum
     // (distr_q.py:449-490), over the compact columns held by lanes 0..w-1 (column order = action
     // order, so the lowest lane among equal values is the first index): column c holds full-row
     // action a(c); every other action of the full row is default_q, the first of them at mind
-    const uint32_t rd = swr.row_desc(slot);
-    const int mind = (int)((rd >> 16) & 15u);
-    const uint32_t a_c = (rd >> (4u * ((uint32_t)lane & 3u))) & 15u;
-    const double NEG = -__builtin_huge_val();
-    const double vq = colv ? v_c : NEG;
-    const double vm = (colv && ((amask >> a_c) & 1u)) ? v_c : NEG;
-    const double mq4 = quad_max(vq), am4 = quad_max(vm);
-    const double mqu = unid(mq4), amu = unid(am4);
-    const int cb = ctz64(__ballot(colv && v_c == mqu));
-    const int ca = ctz64(__ballot(vm == amu && colv && ((amask >> a_c) & 1u)));
-    double mx = __longlong_as_double(((long long)(uint32_t)__builtin_amdgcn_readlane((int)(__double_as_longlong(v_c) >> 32), cb) << 32) |
-                                     (long long)(uint32_t)__builtin_amdgcn_readlane((int)__double_as_longlong(v_c), cb));
-    int best = (int)((rd >> (4 * cb)) & 15u);
-    if (mind != 15 && (m.default_q > mx || (m.default_q == mx && mind < best))) {
-      mx = m.default_q;
-      best = mind;
+    double mx;
+    int best, arg;
+    if (row_hit) {
+      mx = unid(pf_mx);
+      const uint32_t ba = uni((uint32_t)pfd67[0]);
+      best = (int)(ba & 0xFFu);
+      arg = (int)((ba >> 8) & 0xFFu);
+    } else {
+      const uint32_t rd = swr.row_desc(slot);
+      const int mind = (int)((rd >> 16) & 15u);
+      const uint32_t a_c = (rd >> (4u * ((uint32_t)lane & 3u))) & 15u;
+      const double NEG = -__builtin_huge_val();
+      const double vq = colv ? v_c : NEG;
+      const double vm = (colv && ((amask >> a_c) & 1u)) ? v_c : NEG;
+      const double mq4 = quad_max(vq), am4 = quad_max(vm);
+      const double mqu = unid(mq4), amu = unid(am4);
+      const int cb = ctz64(__ballot(colv && v_c == mqu));
+      const int ca = ctz64(__ballot(vm == amu && colv && ((amask >> a_c) & 1u)));
+      mx = __longlong_as_double(((long long)(uint32_t)__builtin_amdgcn_readlane((int)(__double_as_longlong(v_c) >> 32), cb) << 32) |
+                                (long long)(uint32_t)__builtin_amdgcn_readlane((int)__double_as_longlong(v_c), cb));
+      best = (int)((rd >> (4 * cb)) & 15u);
+      if (mind != 15 && (m.default_q > mx || (m.default_q == mx && mind < best))) {
+        mx = m.default_q;
+        best = mind;
+      }
+      arg = (int)((rd >> (4 * ca)) & 15u);
     }
-    const int arg = (int)((rd >> (4 * ca)) & 15u);
     d.mq = mx;
     if (!explore) {
       if (lane == 0) touch_row(prr.row_base() + state);
       action = ((amask >> best) & 1u) ? best : arg;
     }
     if (action < 0 || action >= na) lerr |= E_BAD_ACTION;
+    SFL_LAP(7);
     SFL_PACC(1, t_eg);
     SFL_PT(t_ap);
     // _apply_action
@@ -990,34 +1130,43 @@ struct WEnv {
       }
     }
     int next_sw = sw, target = -1;
+    bool blk_moving = false;
     if (moving) {
       // transition_train / transition_semaphore (rail_network.py:246-278, 303-416)
-      const PortRec po = port_rec(out_p);
-      target = po.nb();
-      const PortRec pt = port_rec(target);
+      const u4 rc = ldcv<u4>(m.port_tr, (size_t)out_p);  // one scalar load for the whole recipe
+      target = (int)(int16_t)(rc[0] & 0xFFFFu);
       if (tb_state(b) != S_MALF) {
         // free the train's records on the ports of its current and previous switch
         const int x1 = pin >> 2;
         const int x2 = pprev != (int)PORT_NONE ? (pprev >> 2) : -1;
-#pragma unroll
-        for (int kk = 0; kk < PPL; ++kk) {
-          const int x = (kk * 64 + lane) >> 2;
-          const uint32_t r = sem(kk);
-          if ((x == x1 || x == x2) && r_present(r) && r_owner(r) == (uint32_t)h) sem(kk) = 0u;
-        }
+        // lanes 0-3: the ports of switch x1, lanes 4-7: those of x2
+        const int xs = lane < 4 ? x1 : x2;
+        const bool act = lane < 8 && xs >= 0;
+        const int pc = act ? 4 * xs + (lane & 3) : 0;
+        const uint32_t r = lsem[pc];
+        if (act && r_present(r) && r_owner(r) == (uint32_t)h) lsem[pc] = 0u;
       }
-      const int32_t d_ot = po.len();
-      put_keep(out_p, h, 0, 3, 0);
-      put_keep(target, h, 1, d_ot + 1, 1);
-      const int u = pt.unique();
-      if (u >= 0) {
-        const PortRec pu = port_rec(u);
-        if (u != in_p && u != out_p && u != target) put_replace(u, h, 0, d_ot + 1, 0);
-        put_replace(u, h, 0, d_ot, -1);
-        const int far = pu.nb();
-        if (far != in_p && far != out_p && far != u) put_replace(far, h, 1, d_ot + pu.len() + 1, 1);
+      // transition_semaphore's record updates on the out, target, unique-onward and far ports,
+      // evaluated on register copies of the four records (one LDS round trip; writes to a port
+      // that appears in several roles update every copy) and written back once
+      const int32_t d_ot = (int32_t)(int16_t)(rc[1] >> 16);
+      const int u = (int)(int16_t)(rc[0] >> 16);
+      const bool hu = u >= 0;
+      const int far = (int)(int16_t)(rc[1] & 0xFFFFu);
+      const int32_t len_u = (int32_t)rc[2];
+      SemQuad q4(lsem, out_p, target, u, far);
+      q4.put(out_p, put_keep_f(h, 0, 3, 0));
+      q4.put(target, put_keep_f(h, 1, d_ot + 1, 1));
+      if (hu) {
+        if (u != in_p && u != out_p && u != target) q4.put(u, put_replace_f(h, 0, d_ot + 1, 0));
+        q4.put(u, put_replace_f(h, 0, d_ot, -1));
+        if (far != in_p && far != out_p && far != u) q4.put(far, put_replace_f(h, 1, d_ot + len_u + 1, 1));
       }
-      if (target != in_p && target != out_p) put_replace(target, h, 0, d_ot + 1, 0);
+      if (target != in_p && target != out_p) q4.put(target, put_replace_f(h, 0, d_ot + 1, 0));
+      q4.store(lane);
+      // check_port_blocked(target, out_p) on the updated records (reward_func.py:62-70)
+      blk_moving = (rec_blocks(q4.v[1], (uint32_t)h, malf, 0u) | rec_blocks(q4.v[0], (uint32_t)h, malf, 1u)) != 0u;
+      SFL_LAP(8);
       tset(sdec, h, (sd & 0xFFFF0000u) | (uint32_t)in_p);
       tset(nprv, h, (uint32_t)target | ((uint32_t)out_p << 16));
       next_sw = target >> 2;
@@ -1035,7 +1184,7 @@ struct WEnv {
     tset(plan, h, p);
     bool all_blocked;
     if (moving) {
-      all_blocked = port_blocked(target, out_p, h);
+      all_blocked = uni((uint32_t)blk_moving) != 0u;
     } else {
       all_blocked = true;  // semaphores unchanged since the observation
       for (int a = 0; a < na - 1; ++a) {
@@ -1045,7 +1194,9 @@ struct WEnv {
     }
     // reward_func.py:23-78: distance at the position projected along the non-STOP plan (staged
     // by prefetch for the STOP plan and for each final rail action of a route)
-    const int32_t cur = now - la + dist_staged(uni(moving ? pfih[2 + (turn & 3u)] : pfih[1]));
+    const uint32_t tq = turn & 3u;
+    const int32_t dproj = moving ? (tq == 0 ? pfd23[0] : tq == 1 ? pfd23[1] : tq == 2 ? pfd45[0] : pfd45[1]) : pfd01[1];
+    const int32_t cur = now - la + dist_staged(uni(dproj));
     const int32_t diff = rl(delay, h) - cur;
     d.r_new = (pl_front(p) == A_STOP && !all_blocked) ? diff - 1300 : diff;
     tset(delay, h, cur);
@@ -1057,6 +1208,7 @@ struct WEnv {
     d.j = (action == stop) ? (w - 1) : swr.j(action);
     d.reward = reward;
     d.next_sw = next_sw;
+    SFL_LAP(9);
     SFL_PACC(2, t_ap);
   }
 
@@ -1064,6 +1216,7 @@ struct WEnv {
   // The (switch, train) slot of the deciding switch is consumed and the successor slot gets
   // the new pending update and the reward the train will see there (AECEnv.last).
   __device__ __forceinline__ void post(const Dec& d, bool greedy) {
+    SFL_LAP0();
     const int T = m.T;
     if (greedy) {
       if (lane == 0) st(slotb, slot_ix(d.next_sw, d.h), slot_make(PEND_NONE, d.r_new, epoch));
@@ -1127,6 +1280,7 @@ struct WEnv {
       }
     }
     cset(d.sw, cget(d.sw) + 1u);
+    SFL_LAP(10);
   }
 
   // order-independent checksum of the semaphore table (trace/debug only)
@@ -1274,6 +1428,7 @@ __device__ void run(const SflMap& m, const SflState& s, const SflCtl& c) {
   if (lane == 0) {
     for (int k = 0; k < 5; ++k) atomicAdd(&g_prof[k], (unsigned long long)prof[k]);
     for (int k = 0; k < 9; ++k) atomicAdd(&g_prof[5 + k], (unsigned long long)v.prof[k]);
+    for (int k = 0; k < 16; ++k) atomicAdd(&g_prof[16 + k], (unsigned long long)v.lap[k]);
   }
 #endif
   if (lane == 0) {
