@@ -74,6 +74,19 @@ __global__ void k_replicate(uint32_t* base, size_t words, uint32_t n) {
     base[words + i] = base[i % words];
 }
 
+// The exploratory action (distr_q.py:315-317) seeds a fresh Generator(PCG64(SeedSequence(v)))
+// with v = rng.integers(0, 2**31 - 1) and draws one bounded integer from it, whose Lemire step
+// needs only the generator's first 32-bit output.  That output is a pure function of v, so it is
+// tabulated once per device for all 2^31 values (8.6 GB of the 288 GB HBM): an exploratory
+// decision then costs one load instead of ~250 dependent integer instructions.
+__global__ void k_seedseq_table(uint32_t* out, uint64_t n) {
+  for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (uint64_t)gridDim.x * blockDim.x) {
+    sfl::Pcg64 g;
+    sfl::pcg_from_seedseq((uint32_t)v, g);
+    out[v] = sfl::pcg_next32(g);
+  }
+}
+
 __global__ void k_fill_f64(double* p, double v, size_t n) {
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) p[i] = v;
 }
@@ -219,6 +232,23 @@ struct HipBackend {
     return err.empty() ? 0 : -1;
   }
   int sync() { return check(hipStreamSynchronize(stream), "sync") && err.empty() ? 0 : -1; }
+  // process-wide, one per device, built on first use and kept for the life of the process
+  const uint32_t* seedseq_table() {
+    static uint32_t* tab[64] = {};
+    if (dev < 0 || dev >= 64) return nullptr;
+    if (!tab[dev]) {
+      const uint64_t n = 1ull << 31;
+      void* p = nullptr;
+      if (hipMalloc(&p, n * 4) != hipSuccess) return nullptr;  // no table: draws fall back to compute
+      k_seedseq_table<<<16384, 256, 0, stream>>>((uint32_t*)p, n);
+      if (!check(hipGetLastError(), "k_seedseq_table") || !check(hipStreamSynchronize(stream), "k_seedseq_table")) {
+        hipFree(p);
+        return nullptr;
+      }
+      tab[dev] = (uint32_t*)p;
+    }
+    return tab[dev];
+  }
   void replicate(void* base, size_t bytes, uint32_t n) {
     if (n > 1) k_replicate<<<4096, 256, 0, stream>>>((uint32_t*)base, bytes / 4, n);
     check(hipGetLastError(), "k_replicate");

@@ -87,6 +87,7 @@ struct SflMap {
   const uint32_t* port_pack;  // [NP][4]: nb | len<<16; unique | q_w<<16; row_base; q_off
   const uint32_t* move_tab;   // [H*W][4 dir][4 action&3]: check_action result (see move_pack)
   const int32_t* tr_pack;     // [T][8]: ed, la, k, target, init_cell, init_dist, init_delay, init_dir | init_port<<16
+  const uint32_t* seedseq32;  // [2^31] first 32-bit output of Generator(PCG64(SeedSequence(v))), or null
   const uint32_t* port_tr;    // [NP][4]: transition recipe of an out port o: nb(o) | unique(nb(o)) << 16;
                               //          nb(unique) | len(o) << 16; len(unique); 0  (int16 fields, -1 = none)
 };

@@ -267,6 +267,7 @@ int create(const sfl_map_desc* md, const sfl_hparams* hp, uint32_t n_envs, const
     m.move_tab = h->upload(h->keep.back().data(), h->keep.back().size());
     h->keep.push_back(std::move(ptr_));
     m.port_tr = h->upload(h->keep.back().data(), h->keep.back().size());
+    m.seedseq32 = h->be.seedseq_table();
     h->keep.emplace_back(trp.begin(), trp.end());
     m.tr_pack = (const int32_t*)h->upload(h->keep.back().data(), h->keep.back().size());
   }

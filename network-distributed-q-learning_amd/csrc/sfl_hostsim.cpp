@@ -55,6 +55,7 @@ struct HostBackend {
     return 0;
   }
   int sync() { return 0; }
+  const uint32_t* seedseq_table() { return nullptr; }  // the host build draws every sub-generator
   void replicate(void* base, size_t bytes, uint32_t n) {
     for (uint32_t i = 1; i < n; ++i) memcpy((char*)base + (size_t)i * bytes, base, bytes);
   }

@@ -1049,9 +1049,8 @@ struct WEnv {
       rng.slo = rng_w[1];
       rng.ihi = rng_w[2];
       rng.ilo = rng_w[3];
-      const uint64_t hb = rng_w[4];
-      rng.has = (uint32_t)(hb >> 32);
-      rng.buf = (uint32_t)hb;
+      rng.has = (uint32_t)(rng_w[4] >> 32);
+      rng.buf = (uint32_t)rng_w[4];
       const uint32_t n = n_sw;
       const double eps = n < (uint32_t)EPS_WIN && n < (uint32_t)m.ntab ? unid(leps[n])
                          : n < (uint32_t)m.ntab                      ? ldc(m.eps_tab, (size_t)n)
@@ -1059,10 +1058,23 @@ struct WEnv {
       if (unid(pcg_double(rng)) < eps) {
         explore = true;
         const uint32_t sub_seed = pcg_bounded(rng, 2147483646u);
-        Pcg64 sub;
-        pcg_from_seedseq(sub_seed, sub);
         const uint32_t nvalid = (uint32_t)__builtin_popcount(amask);
-        const uint32_t pick = pcg_bounded(sub, nvalid - 1u);
+        // Discrete.sample(mask) == valid[default_rng(sub_seed).integers(0, nvalid)]: Lemire on the
+        // sub-generator's first 32-bit output (tabulated, see k_seedseq_table); the rare rejected
+        // draw, and a device without the table, run the sub-generator itself
+        uint32_t pick = 0;
+        bool slow = nvalid > 1u;
+        if (slow && m.seedseq32) {
+          const uint64_t mm = (uint64_t)ldc(m.seedseq32, (size_t)uni(sub_seed)) * nvalid;
+          const uint32_t thr = (0u - nvalid) % nvalid;
+          slow = (uint32_t)mm < thr;
+          pick = (uint32_t)(mm >> 32);
+        }
+        if (slow) {
+          Pcg64 sub;
+          pcg_from_seedseq(sub_seed, sub);
+          pick = pcg_bounded(sub, nvalid - 1u);
+        }
         uint32_t mk = amask;
         for (uint32_t kk = 0; kk < pick; ++kk) mk &= mk - 1u;
         action = __builtin_ctz(mk);
