@@ -45,7 +45,7 @@ constexpr uint32_t PEND_NONE = 0xFFFFFFFFu;
 constexpr uint16_t PORT_NONE = 0xFFFFu;
 
 struct SflMap {
-  int32_t H, W, S, T, K, NP, HW;
+  int32_t H, W, S, T, K, NP, HW, cell_bits;  // cell_bits: bits of a cell index (HW - 1)
   int32_t max_episode_steps, mf_min, mf_max, ntab;
   double mf_rate, gamma, eps0, eps_decay, lr0, lr_decay, default_q;
   int64_t max_steps;

@@ -135,6 +135,8 @@ int create(const sfl_map_desc* md, const sfl_hparams* hp, uint32_t n_envs, const
   m.H = md->H;
   m.W = md->W;
   m.HW = md->H * md->W;
+  m.cell_bits = 1;
+  while ((1 << m.cell_bits) < m.HW) ++m.cell_bits;
   m.S = md->S;
   m.T = md->T;
   m.K = md->K;

@@ -642,19 +642,29 @@ struct WEnv {
     const uint64_t M = __ballot(mover);
     uint64_t A = 0;
     if (M) {
-      bool win = mover;
-      int occ = -1;
-      uint64_t cand_j = M | __ballot(pos >= 0);
-      while (cand_j) {
-        const int j = ctz64(cand_j);
-        cand_j &= cand_j - 1ull;
-        const int32_t dj = rl(desired, j);
-        const int32_t pj = rl(pos, j);
-        if (mover) {
-          if (((M >> j) & 1ull) && j < h && dj == desired) win = false;
-          if (pj >= 0 && pj == desired && j != h) occ = j;
-        }
+      // Bit-sliced equality instead of a loop over trains: for each bit of the cell index, one
+      // ballot of the movers' desired cells and one of the on-map trains' cells; a lane ANDs in
+      // each ballot or its complement by its own desired cell's bit, leaving exactly the movers
+      // that want the same cell (`same`) and the train that occupies it (`occs`).  One extra bit
+      // keeps an off-grid target (-1) apart from every cell.
+      uint64_t same = M, occs = __ballot(mine && pos >= 0);
+      const uint32_t dv = (uint32_t)desired;
+      for (int bi = 0; bi < m.cell_bits; ++bi) {
+        const uint64_t bd = __ballot(mover && ((dv >> bi) & 1u));
+        const uint64_t bp = __ballot(mine && pos >= 0 && (((uint32_t)pos >> bi) & 1u));
+        const bool one = (dv >> bi) & 1u;
+        same &= one ? bd : ~bd;
+        occs &= one ? bp : ~bp;
       }
+      if (m.cell_bits < 32) {  // the sign bit of an off-grid target
+        const uint64_t bd = __ballot(mover && desired < 0);
+        same &= desired < 0 ? bd : ~bd;
+        if (desired < 0) occs = 0;
+      }
+      // the lowest handle wanting a cell wins it; the occupant is the (last) train on it
+      const bool win = mover && !(same & ((1ull << h) - 1ull));
+      const uint64_t occset = occs & ~(1ull << h);
+      const int occ = (mover && occset) ? 63 - __builtin_clzll(occset) : -1;
       while (true) {
         const bool cand = mover && win && !((A >> h) & 1ull) &&
                           (occ < 0 || (((M >> occ) & 1ull) && ((A >> occ) & 1ull)));
