@@ -17,7 +17,7 @@
 #include "sfl_wave.h"
 
 #ifndef SFL_WAVE_OCC
-#define SFL_WAVE_OCC 5  // waves per SIMD the one-env-per-wave kernel is register-budgeted for (5: 96 VGPRs)
+#define SFL_WAVE_OCC 6  // waves per SIMD the one-env-per-wave kernel is register-budgeted for (6: 80 VGPRs)
 #endif
 
 namespace {

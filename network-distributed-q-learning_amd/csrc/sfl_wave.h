@@ -171,8 +171,8 @@ struct WEnv {
   uint32_t sdec;  // source port | decision switch << 16
   int32_t delay;
   // timetable constants of train `lane` (tr_pack)
-  int32_t t_ed, t_target, t_init_cell;
-  uint32_t t_init;  // init dir | init port << 16
+  // timetable constants of the lane's train (tr_pack row) live in LDS and are read where used
+  const int32_t* ltt;  // [TW][8]
   // this env's semaphore records and switch counters in LDS (one region per wave):
   // uniform reads are broadcast ds_reads, writes one lane's ds_write, and the lane-parallel
   // scans read entries k*64 + lane (conflict-free)
@@ -211,6 +211,7 @@ struct WEnv {
   __device__ WEnv(const SflMap& m_, const SflState& s_, uint32_t e_, int lane_, uint32_t* lds, const double* leps_)
       : m(m_), s(s_), e(e_), E(s_.E), lane(lane_), mine(lane_ < m_.T), lsem(lds), lcnt(lds + 64 * PPL), lpf((double*)(lds + 64 * (PPL + SPL))), leps(leps_) {
     lrng = (uint64_t*)(lds + 64 * (PPL + SPL) + TWc * PF_W * 2);
+    ltt = (const int32_t*)(lds + 64 * (PPL + SPL) + TWc * PF_W * 2 + 12);
     qb = s.q + (size_t)e * m.q_per_env;
     pf_ok = false;
     pf_roff = pf_qoff = PF_NONE;
@@ -440,10 +441,8 @@ struct WEnv {
       nprv = (uint32_t)ld(s.tr_next, ix(lane)) | ((uint32_t)ld(s.tr_prev, ix(lane)) << 16);
       sdec = (uint32_t)ld(s.tr_src, ix(lane)) | ((uint32_t)ld(s.tr_dec, ix(lane)) << 16);
       delay = ld(s.tr_delay, ix(lane));
-      t_ed = ld(m.tr_pack, (size_t)lane * 8 + 0);
-      t_target = ld(m.tr_pack, (size_t)lane * 8 + 3);
-      t_init_cell = ld(m.tr_pack, (size_t)lane * 8 + 4);
-      t_init = (uint32_t)ld(m.tr_pack, (size_t)lane * 8 + 7);
+      *(vec_t<int32_t, 4>*)(ltt + 8 * lane) = ld((const vec_t<int32_t, 4>*)m.tr_pack, (size_t)lane * 2u);
+      *(vec_t<int32_t, 4>*)(ltt + 8 * lane + 4) = ld((const vec_t<int32_t, 4>*)m.tr_pack, (size_t)lane * 2u + 1u);
     } else {
       pos = -1;
       bits = 0;
@@ -451,8 +450,6 @@ struct WEnv {
       nprv = 0xFFFFFFFFu;
       sdec = 0xFFFFFFFFu;
       delay = 0;
-      t_ed = t_target = t_init_cell = 0;
-      t_init = 0;
     }
 #pragma unroll
     for (int k = 0; k < PPL; ++k) {
@@ -539,11 +536,12 @@ struct WEnv {
   __device__ __forceinline__ void reset() {
     now = 0;
     if (mine) {
+      const uint32_t t_init = (uint32_t)ltt[8 * lane + 7];
       pos = -1;
       bits = tb_make(t_init & 0xFFu, S_WAITING, A_NONE, 0, 0, 0);
       plan = 0;
       nprv = (nprv & 0xFFFF0000u) | (t_init >> 16);
-      delay = ld(m.tr_pack, (size_t)lane * 8 + 6);
+      delay = ltt[8 * lane + 6];
     }
 #pragma unroll
     for (int k = 0; k < PPL; ++k) sem(k) = 0u;
@@ -574,7 +572,10 @@ struct WEnv {
     const int32_t t = ++now;
     const uint64_t seed = s.seed[e];
     const int h = lane;
-    const uint32_t t_init_dir = t_init & 0xFFu;
+    const vec_t<int32_t, 4> tt0 = *(const vec_t<int32_t, 4>*)(ltt + 8 * (mine ? lane : 0));
+    const vec_t<int32_t, 4> tt1 = *(const vec_t<int32_t, 4>*)(ltt + 8 * (mine ? lane : 0) + 4);
+    const int32_t t_ed = tt0[0], t_target = tt0[3], t_init_cell = tt1[0];
+    const uint32_t t_init_dir = (uint32_t)tt1[3] & 0xFFu;
     // pass 1: plan pop + prediction, malfunction draw, action preprocessing, desired move
     bool mover = false;
     int32_t desired = -1, pred = -1;
@@ -747,7 +748,7 @@ struct WEnv {
     while (D) {
       const int j = ctz64(D);
       D &= D - 1ull;
-      const int32_t ed = rl(t_ed, j);
+      const int32_t ed = ltt[8 * j];
       sset((int)(rl(nprv, j) & 0xFFFFu), r_pack(j, 1, ed - 2, ed + ldc(m.tr_pack, (size_t)j * 8 + 5)));
     }
     // pass 4: extend_semaphores (rail_network.py:229-244)
@@ -827,7 +828,7 @@ struct WEnv {
     const u4 w0 = ld((const u4*)m.sw_pack, (size_t)sw * 4u);
     const u4 w4 = ld((const u4*)m.sw_pack, (size_t)sw * 4u + 1u);  // compact-row descriptors
     const vec_t<uint32_t, 2> nbw = ld((const vec_t<uint32_t, 2>*)m.sw_pack, (size_t)sw * 8u + 4u);
-    const u4 trw = ld((const u4*)m.tr_pack, (size_t)lane * 2u);  // ed, la, k, target
+    const vec_t<int32_t, 4> trw = *(const vec_t<int32_t, 4>*)(ltt + 8 * lane);  // ed, la, k, target
     const u4 pr = ld((const u4*)m.port_pack, (size_t)(4 * sw + slot));
     const uint32_t n_plan = pl_len(plan);
     const uint32_t a1 = n_plan ? pl_front(plan) : A_FWD;
@@ -1324,7 +1325,7 @@ struct WEnv {
 template <int PPL, int SPL, int TW, bool TRACE>
 __device__ void run(const SflMap& m, const SflState& s, const SflCtl& c) {
   using V = WEnv<PPL, SPL, TW>;
-  constexpr int LDS_WORDS = 64 * (PPL + SPL) + TW * PF_W * 2 + 12;  // semaphores, counters, prefetch records, rng
+  constexpr int LDS_WORDS = 64 * (PPL + SPL) + TW * PF_W * 2 + 12 + TW * 8;  // semaphores, counters, prefetch records, rng, timetable
   const int lane = (int)__lane_id();
   const uint32_t e = uni((uint32_t)((blockIdx.x * blockDim.x + threadIdx.x) >> 6));
   __shared__ double leps[EPS_WIN];
