@@ -10,7 +10,7 @@ timeout -k 10 300 python __graft_entry__.py > $OUT/smoke.log 2>&1; echo "smoke r
 timeout -k 10 300 python test_model.py $OUT/test_model --episodes 5 > $OUT/test_model.log 2>&1; echo "test_model rc=$?"; tail -4 $OUT/test_model.log
 timeout -k 10 600 python bench.py --steps 10 --warmup 2 ${BENCH_ARGS} > $OUT/bench.json 2> $OUT/bench.err; echo "bench rc=$?"; cat $OUT/bench.json
 [ -n "$NOPROF" ] && exit 0
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o ktrace --output-format csv -- python bench.py --steps 5 --warmup 1 --no-cpu > $OUT/prof_bench.json 2>/dev/null; echo "ktrace rc=$?"
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o ktrace --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu > $OUT/prof_bench.json 2>/dev/null; echo "ktrace rc=$?"
 for C in FETCH_SIZE WRITE_SIZE "TCC_HIT_sum TCC_MISS_sum" "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_VALU"; do
   N=$(echo $C | tr ' ' '_')
   timeout -k 10 600 rocprofv3 --pmc $C --kernel-trace -d $OUT/pmc_$N -o pmc --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu > /dev/null 2>&1; echo "pmc $N rc=$?"
