@@ -87,6 +87,38 @@ __global__ void k_seedseq_table(uint32_t* out, uint64_t n) {
   }
 }
 
+// per-launch totals of the per-env counters (one block): decisions, ticks, bytes, OR of errors
+__global__ void __launch_bounds__(1024) k_reduce_launch(const uint64_t* dec, const uint64_t* ticks, const uint64_t* bytes,
+                                                        const uint32_t* err, uint32_t E, uint64_t* out) {
+  __shared__ uint64_t red[4][16];
+  uint64_t a = 0, b = 0, c = 0, o = 0;
+  for (uint32_t e = threadIdx.x; e < E; e += blockDim.x) {
+    a += dec[e];
+    b += ticks[e];
+    c += bytes[e];
+    o |= err[e];
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    a += __shfl_xor(a, off, 64);
+    b += __shfl_xor(b, off, 64);
+    c += __shfl_xor(c, off, 64);
+    o |= __shfl_xor(o, off, 64);
+  }
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    red[0][w] = a;
+    red[1][w] = b;
+    red[2][w] = c;
+    red[3][w] = o;
+  }
+  __syncthreads();
+  if (threadIdx.x < 4) {
+    uint64_t t = 0;
+    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) t = threadIdx.x == 3 ? (t | red[3][i]) : t + red[threadIdx.x][i];
+    out[threadIdx.x] = t;
+  }
+}
+
 __global__ void k_fill_f64(double* p, double v, size_t n) {
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) p[i] = v;
 }
@@ -248,6 +280,11 @@ struct HipBackend {
       tab[dev] = (uint32_t*)p;
     }
     return tab[dev];
+  }
+  void reduce_launch(const uint64_t* dec, const uint64_t* ticks, const uint64_t* bytes, const uint32_t* err, uint32_t E,
+                     uint64_t* out) {
+    k_reduce_launch<<<1, 1024, 0, stream>>>(dec, ticks, bytes, err, E, out);
+    check(hipGetLastError(), "k_reduce_launch");
   }
   void replicate(void* base, size_t bytes, uint32_t n) {
     if (n > 1) k_replicate<<<4096, 256, 0, stream>>>((uint32_t*)base, bytes / 4, n);

@@ -35,7 +35,10 @@ struct Handle {
   std::vector<void*> allocs;
   std::vector<uint64_t> seeds;
   // host copies of small per-env counters for reporting
-  std::vector<uint64_t> h_dec, h_ticks, h_bytes;
+  // launch totals reduced on the device (decisions, ticks, algorithmic bytes, OR of error flags)
+  uint64_t last_dec = 0, last_ticks = 0, last_bytes = 0, total_dec = 0;
+  uint32_t last_err = 0;
+  uint64_t* d_sums = nullptr;  // [4]
   uint64_t* d_launch_dec = nullptr;
   uint64_t* d_launch_ticks = nullptr;
   uint64_t* d_launch_bytes = nullptr;
@@ -316,6 +319,7 @@ int create(const sfl_map_desc* md, const sfl_hparams* hp, uint32_t n_envs, const
   h->d_launch_dec = h->template dalloc<uint64_t>(E);
   h->d_launch_ticks = h->template dalloc<uint64_t>(E);
   h->d_launch_bytes = h->template dalloc<uint64_t>(E);
+  h->d_sums = h->template dalloc<uint64_t>(4);
   for (void* p : h->allocs)
     if (!p) {
       delete h;
@@ -429,8 +433,25 @@ int apply_qinit(Handle<B>* h, uint32_t n_rows, const uint32_t* row_port, const u
   return rc ? fail(h->be.error()) : 0;
 }
 
+// per-launch totals: one device reduction and a 32-byte copy instead of per-env arrays
+template <class B>
+int reduce_launch(Handle<B>* h) {
+  uint64_t out[4] = {0, 0, 0, 0};
+  h->be.reduce_launch(h->d_launch_dec, h->d_launch_ticks, h->d_launch_bytes, h->st.err, h->E, h->d_sums);
+  h->be.d2h(out, h->d_sums, sizeof out);
+  if (h->be.sync()) return fail(h->be.error());
+  h->last_dec = out[0];
+  h->last_ticks = out[1];
+  h->last_bytes = out[2];
+  h->last_err = (uint32_t)out[3];
+  h->total_dec += out[0];
+  return 0;
+}
+
 template <class B>
 int check_errors(Handle<B>* h) {
+  if (int rc = reduce_launch(h)) return rc;
+  if (!h->last_err) return 0;
   std::vector<uint32_t> err(h->E);
   h->be.d2h(err.data(), h->st.err, h->E * 4);
   if (h->be.sync()) return fail(h->be.error());

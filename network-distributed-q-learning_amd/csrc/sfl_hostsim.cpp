@@ -56,6 +56,16 @@ struct HostBackend {
   }
   int sync() { return 0; }
   const uint32_t* seedseq_table() { return nullptr; }  // the host build draws every sub-generator
+  void reduce_launch(const uint64_t* dec, const uint64_t* ticks, const uint64_t* bytes, const uint32_t* err, uint32_t E,
+                     uint64_t* out) {
+    out[0] = out[1] = out[2] = out[3] = 0;
+    for (uint32_t e = 0; e < E; ++e) {
+      out[0] += dec[e];
+      out[1] += ticks[e];
+      out[2] += bytes[e];
+      out[3] |= err[e];
+    }
+  }
   void replicate(void* base, size_t bytes, uint32_t n) {
     for (uint32_t i = 1; i < n; ++i) memcpy((char*)base + (size_t)i * bytes, base, bytes);
   }

@@ -938,6 +938,8 @@ struct WEnv {
     uint32_t qoff_pend;  // Q cell (offset in the env's block) of the pending update consumed here, or PF_NONE
     double q_pend;    // its value, loaded during the decision
     uint32_t row_pend;  // key-set row of the pending update
+    uint32_t row_cur;   // key-set row of this decision's observation
+    bool touch_cur;     // greedy choice: insert row_cur into the key set (max_action's __check_entry)
   };
 
   __device__ __forceinline__ void decide(Dec& d, bool greedy) {
@@ -1130,10 +1132,9 @@ struct WEnv {
       arg = (int)((rd >> (4 * ca)) & 15u);
     }
     d.mq = mx;
-    if (!explore) {
-      if (lane == 0) touch_row(prr.row_base() + state);
-      action = ((amask >> best) & 1u) ? best : arg;
-    }
+    d.row_cur = prr.row_base() + state;
+    d.touch_cur = !explore;  // the key-set insert is done by post (one lane-0 region)
+    if (!explore) action = ((amask >> best) & 1u) ? best : arg;
     if (action < 0 || action >= na) lerr |= E_BAD_ACTION;
     SFL_LAP(7);
     SFL_PACC(1, t_eg);
@@ -1242,15 +1243,20 @@ struct WEnv {
     SFL_LAP0();
     const int T = m.T;
     if (greedy) {
-      if (lane == 0) st(slotb, slot_ix(d.next_sw, d.h), slot_make(PEND_NONE, d.r_new, epoch));
+      if (lane == 0) {
+        if (d.touch_cur) touch_row(d.row_cur);
+        st(slotb, slot_ix(d.next_sw, d.h), slot_make(PEND_NONE, d.r_new, epoch));
+      }
       return;
     }
-    if (d.qoff_pend != PF_NONE) {
+    const bool hp = d.qoff_pend != PF_NONE;
+    int ps = 0;
+    double nv = 0.0;
+    if (hp) {
       const uint32_t pend = slot_pend(d.slotword, epoch);
-      const int ps = (int)(pend & 0xFFFu);
+      ps = (int)(pend & 0xFFFu);
       const double lr = lr_of(cget(ps));
       const double r = (double)d.reward;
-      double nv;
       if (d.sw != ps) {
         const double a1 = (1.0 - lr) * d.q_pend;
         const double b1 = lr * (r + m.gamma * d.mq);
@@ -1260,18 +1266,19 @@ struct WEnv {
         const double b1 = lr * r;
         nv = a1 + b1;
       }
-      if (lane == 0) {
+    }
+    // every global write of the step from one lane-0 region
+    if (lane == 0) {
+      if (hp) {
         st(qbase(), (size_t)d.qoff_pend, nv);
         touch_row(d.row_pend);
-        if (d.sw != ps) touch_row(port_rec(4 * d.sw + d.slot).row_base() + d.state);
       }
-      pf_written(d.qoff_pend);
-    }
-    if (lane == 0) {
+      if (d.touch_cur || (hp && d.sw != ps)) touch_row(d.row_cur);
       st(slotb, slot_ix(d.sw, d.h), slot_make(PEND_NONE, slot_rew(d.slotword, epoch), epoch));
       st(slotb, slot_ix(d.next_sw, d.h),
          slot_make(pend_make((uint32_t)d.sw, (uint32_t)d.slot, d.state, (uint32_t)d.j), d.r_new, epoch));
     }
+    if (hp) pf_written(d.qoff_pend);
     // destination bonus for newly arrived trains (distr_q.py:344-356); lanes take switches.
     // Distinct slots of one train never hold the same Q cell (same cell => same action =>
     // same successor switch => same slot), so the lanes' updates are independent.
@@ -1345,6 +1352,8 @@ __device__ void run(const SflMap& m, const SflState& s, const SflCtl& c) {
   d.mq = d.q_pend = 0.0;
   d.qoff_pend = PF_NONE;
   d.row_pend = 0;
+  d.row_cur = 0;
+  d.touch_cur = false;
   const bool test_mode = c.mode == 1;
 #ifdef SFL_PROFILE
   uint64_t prof[5] = {0, 0, 0, 0, 0};
