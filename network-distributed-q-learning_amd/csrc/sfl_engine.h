@@ -248,7 +248,14 @@ int create(const sfl_map_desc* md, const sfl_hparams* hp, uint32_t n_envs, const
     for (size_t c = 0; c < HW; ++c)
       for (int d = 0; d < 4; ++d)
         for (int a = 0; a < 4; ++a)
-          mv[(c * 4 + d) * 4 + a] = move_pack(md->grid, md->H, md->W, (uint32_t)a, (int)c, d);
+        {
+          // bits 24-31: the switch at the destination cell (0xFF: none, or more than 254 switches)
+          uint32_t w = move_pack(md->grid, md->H, md->W, (uint32_t)a, (int)c, d);
+          const int nc = (int)(w & 0xFFFFFu) - 1;
+          const int swd = nc >= 0 ? md->cell_sw[nc] : -1;
+          w |= (uint32_t)(swd >= 0 && md->S <= 254 ? swd : 0xFF) << 24;
+          mv[(c * 4 + d) * 4 + a] = w;
+        }
     for (size_t t = 0; t < T; ++t) {
       int32_t* w = &trp[t * 8];
       w[0] = md->tr_ed[t];

@@ -250,6 +250,7 @@ struct WEnv {
   struct Move {
     int cell, dir;
     bool valid, cell_ok;
+    int sw;  // switch at the destination cell; -1: none; 0xFF: not packed (look it up)
   };
   __device__ __forceinline__ static Move unpack_move(uint32_t w) {
     Move mv;
@@ -257,7 +258,13 @@ struct WEnv {
     mv.dir = (int)((w >> 20) & 3u);
     mv.valid = (w >> 22) & 1u;
     mv.cell_ok = (w >> 23) & 1u;
+    mv.sw = (int)(w >> 24);
     return mv;
+  }
+  // cell_sw of a move's destination cell (packed in the move table when the map has <= 254 switches)
+  __device__ __forceinline__ int dest_sw(const Move& mv) const {
+    if (m.S <= 254) return mv.sw == 0xFF ? -1 : mv.sw;
+    return mv.cell >= 0 ? (int)ld(m.cell_sw, (size_t)mv.cell) : -1;
   }
   // flatland-lite check_action_on_agent as a table lookup; U: wave-uniform arguments (scalar load)
   template <bool U>
@@ -586,6 +593,14 @@ struct WEnv {
       uint32_t st_ = tb_state(b), dir = tb_dir(b), prev = tb_prev(b), saved = tb_saved(b), mf = tb_mf(b);
       uint32_t given = A_NOTHING;
       pred = p0;
+      // every check_action of this pass is at (pc, pd): one 16-byte load of the move-table row
+      const int pc = p0 >= 0 ? p0 : t_init_cell;
+      const int pd = p0 >= 0 ? (int)dir : (int)t_init_dir;
+      const u4 mrow = ld((const u4*)m.move_tab, (size_t)((uint32_t)pc * 4u + (uint32_t)pd));
+      auto mv_of = [&](uint32_t a) -> Move {
+        const uint32_t k = a & 3u;
+        return unpack_move(k == 0 ? mrow[0] : k == 1 ? mrow[1] : k == 2 ? mrow[2] : mrow[3]);
+      };
       if (!tb_done(b)) {
         const uint32_t pl = plan;
         if (pl_len(pl) == 0) {
@@ -596,11 +611,12 @@ struct WEnv {
           plan = pl_pop(pl);
         }
         if (p0 >= 0) {
-          Move mv = check_action<false>(given, p0, (int)dir);
+          const Move mv = mv_of(given);
           aux |= 1u << 12;
           if (mv.valid) {
             aux |= 1u << 13;
             pred = mv.cell;
+            if (dest_sw(mv) >= 0) aux |= 1u << 14;  // the predicted cell is a switch cell
           }
         }
       }
@@ -614,10 +630,14 @@ struct WEnv {
       uint32_t pa = given;
       if (pa == A_NOTHING && st_ == S_MOVING) pa = A_FWD;
       if (st_ == S_WAITING) pa = A_NOTHING;
-      const int pc = p0 >= 0 ? p0 : t_init_cell;
-      const int pd = p0 >= 0 ? (int)dir : (int)t_init_dir;
-      if ((pa == A_LEFT || pa == A_RIGHT) && !action_ok<false>(pa, pc, pd)) pa = A_FWD;
-      if (is_moving_action(pa) && !action_ok<false>(pa, pc, pd)) pa = A_STOP;
+      if (pa == A_LEFT || pa == A_RIGHT) {
+        const Move mv = mv_of(pa);
+        if (!(mv.cell_ok && mv.valid)) pa = A_FWD;
+      }
+      if (is_moving_action(pa)) {
+        const Move mv = mv_of(pa);
+        if (!(mv.cell_ok && mv.valid)) pa = A_STOP;
+      }
       if (is_moving_action(pa) && saved == 0 && st_ != S_DONE) saved = pa;
       const bool update_allowed = (mf == 0) && pa != A_STOP;
       desired = p0;
@@ -628,7 +648,7 @@ struct WEnv {
         ddir = t_init_dir;
         mover = true;
       } else if (saved != 0 && update_allowed) {
-        Move mv = check_action<false>(saved, p0, (int)dir);
+        const Move mv = mv_of(saved);
         desired = mv.cell;
         ddir = (uint32_t)mv.dir;
         pa = saved;
@@ -728,7 +748,7 @@ struct WEnv {
         const uint32_t given = (aux >> 8) & 15u;
         if (pred != np && ((aux >> 13) & 1u) && given != A_STOP) {
           plan = pl_push_front(plan, given, lerr);
-          if (ld(m.cell_sw, (size_t)pred) >= 0) nprv = (nprv & 0xFFFF0000u) | (sdec & 0xFFFFu);
+          if ((aux >> 14) & 1u) nprv = (nprv & 0xFFFF0000u) | (sdec & 0xFFFFu);
         }
       }
       dep = t == t_ed - 2;
@@ -777,9 +797,9 @@ struct WEnv {
     bool act = false;
     if (mine && pos >= 0 && st4 != S_WAITING) {
       const uint32_t nxt = pl_len(plan) ? pl_front(plan) : A_FWD;
-      Move mv = check_action<false>(nxt, pos, (int)tb_dir(bits));
+      const Move mv = check_action<false>(nxt, pos, (int)tb_dir(bits));
       if (mv.cell >= 0) {
-        const int sw_at = ld(m.cell_sw, (size_t)mv.cell);
+        const int sw_at = dest_sw(mv);
         if (sw_at >= 0) {
           int sw = -1;
           if (st4 == S_READY || st4 == S_MOVING) sw = sw_at;
