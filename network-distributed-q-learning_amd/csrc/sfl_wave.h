@@ -852,26 +852,47 @@ struct WEnv {
     const u4 pr = ld((const u4*)m.port_pack, (size_t)(4 * sw + slot));
     const uint32_t n_plan = pl_len(plan);
     const uint32_t a1 = n_plan ? pl_front(plan) : A_FWD;
-    const Move m1 = check_action<false>(a1, pos0, dir0);  // projection of a route: first rail action
+    // move-table rows (all four rail actions) at the cell and after the first rail action
+    const u4 row0 = ld((const u4*)m.move_tab, (size_t)((uint32_t)pos0 * 4u + (uint32_t)dir0));
+    auto mv_in = [](const u4& r, uint32_t a) -> Move {
+      const uint32_t q = a & 3u;
+      return unpack_move(q == 0 ? r[0] : q == 1 ? r[1] : q == 2 ? r[2] : r[3]);
+    };
     // distances the decision needs (reward_func.py:23-78): at the cell, along the STOP plan
-    // ([STOP] + plan) and along each route's plan ([front or FWD, final rail action 0..3])
+    // ([STOP] + plan) and along each route's plan ([front or FWD, final rail action 1..3])
     const int32_t la = (int32_t)trw[1], k = (int32_t)trw[2];
     const int32_t dd = dist_v(k, pos, dir0);
     {
       int pc = pos, pd = dir0;
-      for (uint32_t i = 0; i < n_plan; ++i) project(pl_at(plan, i), pc, pd);
+      for (uint32_t i = 0; i < n_plan; ++i) {
+        const uint32_t a = pl_at(plan, i);
+        if (i == 0 && a != A_STOP && pc >= 0) {
+          const Move mv = mv_in(row0, a);
+          pc = mv.cell;
+          pd = mv.dir;
+        } else {
+          project(a, pc, pd);
+        }
+      }
       pfi[1] = dist_v(k, pc, pd);
     }
     {
       int pc = pos, pd = dir0;
       if (a1 != A_STOP && pos >= 0) {
+        const Move m1 = mv_in(row0, a1);
         pc = m1.cell;
         pd = m1.dir;
       }
+      const u4 row1 = ld((const u4*)m.move_tab, (size_t)((uint32_t)(pc >= 0 ? pc : 0) * 4u + (uint32_t)pd));
+      pfi[2] = 0;  // final rail action 0 (DO_NOTHING) is never a route's
 #pragma unroll
-      for (uint32_t t = 0; t < 4; ++t) {
+      for (uint32_t t = 1; t < 4; ++t) {
         int qc = pc, qd = pd;
-        project(t, qc, qd);
+        if (pc >= 0) {
+          const Move mv = mv_in(row1, t);
+          qc = mv.cell;
+          qd = mv.dir;
+        }
         pfi[2 + t] = dist_v(k, qc, qd);
       }
     }
