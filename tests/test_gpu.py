@@ -167,3 +167,30 @@ def test_partitioned_rounds_gpu_equal_fused(lib, cfg, E):
         assert np.array_equal(q, qr) and np.array_equal(t, tr), f"env {e}"
     pb.close()
     ref.close()
+
+
+@pytest.mark.parametrize("S,T,variant", [(64, 48, 3), (100, 48, 4), (120, 64, 4)])
+def test_wave_kernel_shapes(lib, S, T, variant):
+    """Every k_wave shape (sfl::kVariants: more trains per env, more ports / switches per lane)
+    bit-equal to the host build of the lane kernel, and sampled envs to the oracle."""
+    from tests import hostsim
+    sc = mapgen.generate(S, T, 8, seed=4242, malfunction=(0.01, 5, 15), name="shape")
+    cm = comp.compile_scenario(sc)
+    seeds = [300 + i for i in range(64)]
+    bg = runtime.Batch(cm, HP, seeds, lib=lib, ntab=1 << 14)
+    assert bg.counters()["kernel_variant"] == variant
+    bh = runtime.Batch(cm, HP, seeds, lib=hostsim.lib(), ntab=1 << 14)
+    for b in (bg, bh):
+        b.learn_begin()
+        b.apply_qinit()
+        for n in (50, 130):
+            b.step(n)
+    for e in range(len(seeds)):
+        qg, tg = bg.q_raw(e)
+        qh, th = bh.q_raw(e)
+        assert np.array_equal(qg, qh) and np.array_equal(tg, th), f"env {e}"
+    env, model = so.build(sc, seeds[5], HP, trace=False)
+    so.run_decisions(model, 180)
+    assert bg.q_dict(5) == model.q
+    bg.close()
+    bh.close()
