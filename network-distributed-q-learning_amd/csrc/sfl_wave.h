@@ -981,6 +981,7 @@ struct WEnv {
     uint32_t row_pend;  // key-set row of the pending update
     uint32_t row_cur;   // key-set row of this decision's observation
     bool touch_cur;     // greedy choice: insert row_cur into the key set (max_action's __check_entry)
+    uint32_t abytes;    // algorithmic bytes of the decision
   };
 
   __device__ __forceinline__ void decide(Dec& d, bool greedy) {
@@ -1273,6 +1274,7 @@ struct WEnv {
     d.j = (action == stop) ? (w - 1) : swr.j(action);
     d.reward = reward;
     d.next_sw = next_sw;
+    d.abytes = 220u + 48u * (uint32_t)np + 8u * (uint32_t)na;  // SURVEY.md §8(d) bytes of this decision
     SFL_LAP(9);
     SFL_PACC(2, t_ap);
   }
@@ -1395,7 +1397,9 @@ __device__ void run(const SflMap& m, const SflState& s, const SflCtl& c) {
   d.row_pend = 0;
   d.row_cur = 0;
   d.touch_cur = false;
+  d.abytes = 0;
   const bool test_mode = c.mode == 1;
+  const int64_t max_steps = m.max_steps, dec_budget = c.dec_budget;
 #ifdef SFL_PROFILE
   uint64_t prof[5] = {0, 0, 0, 0, 0};
   const uint64_t t_begin = (uint64_t)__builtin_amdgcn_s_memtime();
@@ -1424,19 +1428,9 @@ __device__ void run(const SflMap& m, const SflState& s, const SflCtl& c) {
       if (v.flags & F_TERM) phase = (v.flags & F_INFLIGHT) ? PH_POST : PH_END;
       else if (v.q_mask) phase = (v.flags & F_INFLIGHT) ? PH_POST : PH_DECIDE;
     } else if (phase == PH_DECIDE || phase == PH_POST) {
-      bool post_now = phase == PH_POST;
       const bool greedy = (v.flags & F_GREEDY) != 0;
-      if (phase == PH_DECIDE) {
-        SFL_PT(t0);
-        v.decide(d, greedy);
-        SFL_PACC(2, t0);
-        const uint32_t w0 = ldc(m.sw_pack, (size_t)d.sw * 16);
-        abytes += 220u + 48u * (w0 & 15u) + 8u * ((w0 >> 4) & 15u);
-        v.flags |= F_INFLIGHT;
-        if (!v.q_mask) phase = PH_TICK;  // ticks happen between the step and the update
-        else post_now = true;
-      }
-      if (post_now) {
+      // post step + loop bookkeeping of decision d; true: the launch's decision budget is spent
+      auto finish = [&]() -> bool {
         SFL_PT(t0);
         v.post(d, greedy);
         SFL_PACC(3, t0);
@@ -1460,10 +1454,31 @@ __device__ void run(const SflMap& m, const SflState& s, const SflCtl& c) {
         v.ep_dec += 1;
         v.n_dec += 1;
         v.step_ctr += 1;
-        if (v.step_ctr > m.max_steps) v.flags |= F_TRUNC;
+        if (v.step_ctr > max_steps) v.flags |= F_TRUNC;
         phase = (v.flags & (F_TERM | F_TRUNC)) ? PH_END : PH_DECIDE;
-        if (c.dec_budget > 0 && (int64_t)v.n_dec >= c.dec_budget) break;
+        return dec_budget > 0 && (int64_t)v.n_dec >= dec_budget;
+      };
+      if (phase == PH_POST) {
+        if (finish()) break;
+        continue;
       }
+      // a batch of queued decisions: decide, and post each one while more are queued (the last
+      // one is posted after the ticks that follow it, switch_env.py:418-421 / distr_q.py:322-343)
+      bool stop = false;
+      while (true) {
+        SFL_PT(t0);
+        v.decide(d, greedy);
+        SFL_PACC(2, t0);
+        abytes += d.abytes;
+        v.flags |= F_INFLIGHT;
+        if (!v.q_mask) {
+          phase = PH_TICK;
+          break;
+        }
+        stop = finish();
+        if (stop || phase != PH_DECIDE) break;
+      }
+      if (stop) break;
     } else {  // PH_END
       const int arrived = popc64(v.arr_mask);
       const size_t cap = (size_t)(c.stats_cap > 0 ? c.stats_cap : 1);
