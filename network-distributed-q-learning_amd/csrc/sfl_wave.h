@@ -1458,23 +1458,23 @@ __device__ void run(const SflMap& m, const SflState& s, const SflCtl& c) {
         phase = (v.flags & (F_TERM | F_TRUNC)) ? PH_END : PH_DECIDE;
         return dec_budget > 0 && (int64_t)v.n_dec >= dec_budget;
       };
-      if (phase == PH_POST) {
-        if (finish()) break;
-        continue;
-      }
       // a batch of queued decisions: decide, and post each one while more are queued (the last
-      // one is posted after the ticks that follow it, switch_env.py:418-421 / distr_q.py:322-343)
-      bool stop = false;
+      // one is posted after the ticks that follow it, switch_env.py:418-421 / distr_q.py:322-343);
+      // PH_POST enters at that deferred post
+      bool stop = false, do_decide = phase == PH_DECIDE;
       while (true) {
-        SFL_PT(t0);
-        v.decide(d, greedy);
-        SFL_PACC(2, t0);
-        abytes += d.abytes;
-        v.flags |= F_INFLIGHT;
-        if (!v.q_mask) {
-          phase = PH_TICK;
-          break;
+        if (do_decide) {
+          SFL_PT(t0);
+          v.decide(d, greedy);
+          SFL_PACC(2, t0);
+          abytes += d.abytes;
+          v.flags |= F_INFLIGHT;
+          if (!v.q_mask) {
+            phase = PH_TICK;
+            break;
+          }
         }
+        do_decide = true;
         stop = finish();
         if (stop || phase != PH_DECIDE) break;
       }
