@@ -31,7 +31,7 @@ def _stale(out: str, srcs) -> bool:
 
 def build_hip(force: bool = False, verbose: bool = False, out: str = None, defines=(), flags=()) -> str:
     """hipcc build of libsfl.so (gfx950).  ``out``/``defines``/``flags``: alternative builds for tuning."""
-    out = out or os.path.join(HERE, "libsfl.so")
+    out = os.path.abspath(out or os.path.join(HERE, "libsfl.so"))
     if force or _stale(out, SOURCES):
         cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off",
                "-Wno-unused-result", "-Wno-unused-value"] + [f"-D{d}" for d in defines] + list(flags) + [
