@@ -44,6 +44,32 @@ def cpu_baseline(sc, seconds: float):
                        f"(from episode start, incl. the Q-table init)")
 
 
+def cpu_cxx_baseline(cm, seconds: float):
+    """The build's C++ CPU backend: the same kernel body compiled for the host
+    (libsfl_hostsim.so, one env per OpenMP thread at a time) on the host cores, same map and
+    hyper-parameters, learning mode.  Reported beside cpu_baseline; not the product path."""
+    build = importlib.import_module(PKG + ".build")
+    _lib = importlib.import_module(PKG + "._lib")
+    runtime = importlib.import_module(PKG + ".runtime")
+    threads = int(os.environ.get("OMP_NUM_THREADS") or 0) or len(os.sched_getaffinity(0))
+    threads = max(1, min(threads, len(os.sched_getaffinity(0)), 16))
+    lib = _lib.Lib(build.build_hostsim())
+    E = 4 * threads
+    b = runtime.Batch(cm, HP, [450565 + i for i in range(E)], lib=lib)
+    b.learn_begin()
+    b.apply_qinit()
+    b.step(64)
+    n = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        n += b.step(64)[0]
+    dt = time.perf_counter() - t0
+    b.close()
+    return dict(value=n / dt, unit="agent-env-steps/sec", cores=threads, kind="port",
+                sample=f"libsfl_hostsim.so (the kernel body built for the host, OpenMP over {E} envs of the c3 map), "
+                       f"{n} decisions in {dt:.1f} s after one untimed 64-decision step")
+
+
 def pmc_traffic():
     """HBM bytes per env-kernel launch from the committed rocprofv3 PMC summary of this exact kernel source
     (profiles/*_pmc.json written by scripts/pmc_summary.py), or None."""
@@ -151,6 +177,7 @@ def main():
         }
         if world == 1 and not args.no_cpu:
             res["cpu_baseline"] = cpu_baseline(sc, args.cpu_seconds)
+            res["cpu_cxx_baseline"] = cpu_cxx_baseline(cm, args.cpu_seconds)
         print(json.dumps(res), flush=True)
     b.close()
     if dist is not None:

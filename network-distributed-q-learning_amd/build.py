@@ -44,8 +44,10 @@ def build_hip(force: bool = False, verbose: bool = False, out: str = None, defin
 
 
 def build_hostsim(out_dir: str = None, force: bool = False) -> str:
-    """TEST ONLY: the same kernel body compiled for the host CPU (libsfl_hostsim.so)."""
-    out_dir = out_dir or os.path.join(HERE, "..", "build")
+    """The same kernel body compiled for the host CPU (libsfl_hostsim.so, OpenMP over envs): the
+    parity tests' host build and bench.py's C++ CPU baseline leg -- never the product path.  Built
+    in-tree so that it travels to the GPU box with the snapshot."""
+    out_dir = out_dir or HERE
     os.makedirs(out_dir, exist_ok=True)
     out = os.path.abspath(os.path.join(out_dir, "libsfl_hostsim.so"))
     if force or _stale(out, SOURCES):

@@ -429,7 +429,12 @@ struct WEnv {
 
   // ---- Q-table ------------------------------------------------------------------------------
   __device__ __forceinline__ double* qbase() const { return qb; }
-  __device__ __forceinline__ void touch_row(uint32_t row) const { atomicOr(&touchb[row >> 5], 1u << (row & 31u)); }
+  // global-address-space atomic: a flat atomic would also count on lgkmcnt, so the decision's next
+  // LDS read or scalar load would wait for its L2 round trip
+  __device__ __forceinline__ void touch_row(uint32_t row) const {
+    __hip_atomic_fetch_or((SFL_AS_G uint32_t*)touchb + (row >> 5), 1u << (row & 31u), __ATOMIC_RELAXED,
+                          __HIP_MEMORY_SCOPE_AGENT);
+  }
   __device__ __forceinline__ double lr_of(uint32_t n) const {
     if (m.lr_decay == 1.0) return m.lr0;  // lr0 * 1.0**n (distr_q.py:70-79)
     return n < (uint32_t)m.ntab ? ldc(m.lr_tab, (size_t)n) : m.lr0 * pow_ool(m.lr_decay, (double)n);
