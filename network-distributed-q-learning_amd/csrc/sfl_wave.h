@@ -50,7 +50,10 @@ constexpr uint32_t PF_NONE = 0xFFFFFFFFu;
 // projected cell if it stops (reward of STOP), if it moves with final rail action 0..3 (reward of
 // a route), and the row's argmax | first allowed argmax << 8 under the staged observation
 constexpr int PF_W = 12, PF_I = 14;
-constexpr int EPS_WIN = 512;  // epsilon table entries kept in LDS
+#ifndef SFL_EPS_WIN
+#define SFL_EPS_WIN 512
+#endif
+constexpr int EPS_WIN = SFL_EPS_WIN;  // epsilon table entries kept in LDS
 constexpr int32_t PF_OFFGRID = (int32_t)0x80000000;  // projection left the grid
 
 #define SFL_AS_G __attribute__((address_space(1)))
