@@ -228,12 +228,12 @@ struct WEnv {
   // ---- cross-lane access (index wave-uniform) -------------------------------------
   __device__ __forceinline__ uint32_t sget(int p) const { return uni(lsem[p]); }
   __device__ __forceinline__ void sset(int p, uint32_t r) {
-    if (lane == 0) lsem[p] = r;
+    lsem[p] = r;  // wave-uniform value from every lane (one address): no lane-0 exec region
   }
   __device__ __forceinline__ uint32_t& sem(int k) const { return lsem[k * 64 + lane]; }  // lane-parallel
   __device__ __forceinline__ uint32_t cget(int sw) const { return uni(lcnt[sw]); }
   __device__ __forceinline__ void cset(int sw, uint32_t v) {
-    if (lane == 0) lcnt[sw] = v;
+    lcnt[sw] = v;  // wave-uniform value from every lane
   }
   __device__ __forceinline__ uint32_t cget_var(int sw) const { return lcnt[sw]; }  // per-lane index
   template <class T>
@@ -409,8 +409,8 @@ struct WEnv {
 #pragma unroll
       for (int i = 0; i < 4; ++i) v[i] = (p[i] == port) ? nv : v[i];
     }
-    __device__ __forceinline__ void store(int lane) const {
-      if (lane == 0) {
+    __device__ __forceinline__ void store() const {  // uniform values, written by every lane
+      {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
           if (p[i] >= 0) l[p[i]] = v[i];
@@ -938,27 +938,29 @@ struct WEnv {
     {
       const uint32_t rd = w4[slot];
       const int na = (int)((w0[0] >> 4) & 15u);
+      // branch-free (selects, fixed trip counts): the lanes of a batch sit on different switches
       uint32_t am = 1u << (na - 1);
-      for (int a = 0; a < na - 1; ++a)
-        if ((int)((w0[1] >> (2 * a)) & 3u) == slot && ((fb >> ((w0[1] >> (16 + 2 * a)) & 3u)) & 1u)) am |= 1u << a;
+#pragma unroll
+      for (int a = 0; a < 8; ++a) {
+        const bool ok = a < na - 1 && (int)((w0[1] >> (2 * a)) & 3u) == slot &&
+                        ((fb >> ((w0[1] >> (16 + 2 * a)) & 3u)) & 1u);
+        am |= ok ? (1u << a) : 0u;
+      }
       const int mind = (int)((rd >> 16) & 15u);
       double mx = mind != 15 ? m.default_q : -__builtin_huge_val();
       int best = mind != 15 ? mind : 99, arg = -1;
       double amx = 0.0;
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
-        if ((uint32_t)c < w) {
-          const int a = (int)((rd >> (4 * c)) & 15u);
-          const double v = rv[c];
-          if (v > mx || (v == mx && a < best)) {
-            mx = v;
-            best = a;
-          }
-          if (((am >> a) & 1u) && (arg < 0 || v > amx || (v == amx && a < arg))) {
-            arg = a;
-            amx = v;
-          }
-        }
+        const int a = (int)((rd >> (4 * c)) & 15u);
+        const double v = rv[c];
+        const bool in = (uint32_t)c < w;
+        const bool b1 = in && (v > mx || (v == mx && a < best));
+        mx = b1 ? v : mx;
+        best = b1 ? a : best;
+        const bool b2 = in && ((am >> a) & 1u) && (arg < 0 || v > amx || (v == amx && a < arg));
+        arg = b2 ? a : arg;
+        amx = b2 ? v : amx;
       }
       pfl[6] = mx;
       pfi[6] = (best & 0xFF) | ((arg & 0xFF) << 8);
@@ -1142,7 +1144,7 @@ struct WEnv {
         for (uint32_t kk = 0; kk < pick; ++kk) mk &= mk - 1u;
         action = __builtin_ctz(mk);
       }
-      if (lane == 0) {
+      {  // uniform values, written by every lane
         lrng[0] = rng.shi;
         lrng[1] = rng.slo;
         lrng[4] = ((uint64_t)rng.has << 32) | rng.buf;
@@ -1237,7 +1239,7 @@ struct WEnv {
         if (far != in_p && far != out_p && far != u) q4.put(far, put_replace_f(h, 1, d_ot + len_u + 1, 1));
       }
       if (target != in_p && target != out_p) q4.put(target, put_replace_f(h, 0, d_ot + 1, 0));
-      q4.store(lane);
+      q4.store();
       // check_port_blocked(target, out_p) on the updated records (reward_func.py:62-70)
       blk_moving = (rec_blocks(q4.v[1], (uint32_t)h, malf, 0u) | rec_blocks(q4.v[0], (uint32_t)h, malf, 1u)) != 0u;
       SFL_LAP(8);
