@@ -294,11 +294,11 @@ struct WEnv {
   // per-lane projection step of reward_func.py:41-56 (STOP entries are skipped, and a cell off
   // the grid ends the walk) and distance lookup with the off-grid marker
   __device__ __forceinline__ void project(uint32_t a, int& pc, int& pd) const {
-    if (a != A_STOP && pc >= 0) {
-      const Move mv = check_action<false>(a, pc, pd);
-      pc = mv.cell;
-      pd = mv.dir;
-    }
+    // lane-parallel (prefetch): a clamped lookup and selects instead of a divergent branch
+    const bool go = (a != A_STOP) & (pc >= 0);
+    const Move mv = check_action<false>(a, pc >= 0 ? pc : 0, pd);
+    pc = go ? mv.cell : pc;
+    pd = go ? mv.dir : pd;
   }
   __device__ __forceinline__ int32_t dist_v(int k, int cell, int dir) const {
     const int32_t d = ld(m.dist, ((uint32_t)k * (uint32_t)m.HW + (uint32_t)(cell >= 0 ? cell : 0)) * 4u + (uint32_t)dir);
@@ -374,11 +374,12 @@ struct WEnv {
     int32_t now, span, ovr;  // ovr: in-flag that is overridden (-1: none)
     bool keep;               // put_keep: an overridden record keeps its in-flag
     __device__ __forceinline__ uint32_t operator()(uint32_t r) const {
+      // selects on bitwise conditions: the record copies live in VGPRs, so a short-circuit
+      // condition would become an exec-mask region
       const uint32_t nr = r_pack(h, keep ? r_in(r) : in, now, now + span);
       const uint32_t fresh = r_pack(h, in, now, now + span);
-      if (!r_present(r)) return fresh;
-      if ((ovr >= 0 && r_in(r) == (uint32_t)ovr) || r_t0(r) > now) return nr;
-      return r;
+      const bool retime = ((ovr >= 0) & (r_in(r) == (uint32_t)ovr)) | (r_t0(r) > now);
+      return !r_present(r) ? fresh : (retime ? nr : r);
     }
   };
   __device__ __forceinline__ PutF put_keep_f(int h, uint32_t in, int32_t span, uint32_t ovr_in) const {
@@ -768,8 +769,10 @@ struct WEnv {
     const uint64_t DONE = __ballot(done);
     if (DONE) {
 #pragma unroll
-      for (int k = 0; k < PPL; ++k)
-        if (r_present(sem(k)) && ((DONE >> r_owner(sem(k))) & 1ull)) sem(k) = 0u;
+      for (int k = 0; k < PPL; ++k) {
+        const uint32_t r = sem(k);
+        sem(k) = (r_present(r) & (((DONE >> r_owner(r)) & 1ull) != 0ull)) ? 0u : r;
+      }
     }
     // departure semaphores, in handle order (switch_env.py:379-384)
     uint64_t D = __ballot(dep);
@@ -786,7 +789,8 @@ struct WEnv {
 #pragma unroll
       for (int k = 0; k < PPL; ++k) {
         const uint32_t r = sem(k);
-        if (r_present(r) && ((SM >> r_owner(r)) & 1ull)) sem(k) = r_pack(r_owner(r), r_in(r), t, t + (r_t1(r) - r_t0(r)));
+        const bool ext = r_present(r) & (((SM >> r_owner(r)) & 1ull) != 0ull);
+        sem(k) = ext ? r_pack(r_owner(r), r_in(r), t, t + (r_t1(r) - r_t0(r))) : r;
       }
     }
     uint64_t MA = __ballot(mine && st4 == S_MALF);
@@ -942,9 +946,9 @@ struct WEnv {
       uint32_t am = 1u << (na - 1);
 #pragma unroll
       for (int a = 0; a < 8; ++a) {
-        const bool ok = a < na - 1 && (int)((w0[1] >> (2 * a)) & 3u) == slot &&
-                        ((fb >> ((w0[1] >> (16 + 2 * a)) & 3u)) & 1u);
-        am |= ok ? (1u << a) : 0u;
+        const uint32_t ok = (uint32_t)(a < na - 1) & (uint32_t)((int)((w0[1] >> (2 * a)) & 3u) == slot) &
+                            ((fb >> ((w0[1] >> (16 + 2 * a)) & 3u)) & 1u);
+        am |= ok << a;
       }
       const int mind = (int)((rd >> 16) & 15u);
       double mx = mind != 15 ? m.default_q : -__builtin_huge_val();
@@ -955,10 +959,11 @@ struct WEnv {
         const int a = (int)((rd >> (4 * c)) & 15u);
         const double v = rv[c];
         const bool in = (uint32_t)c < w;
-        const bool b1 = in && (v > mx || (v == mx && a < best));
+        // bitwise, not short-circuit, operators: no divergent branches in this lane-parallel code
+        const bool b1 = in & ((v > mx) | ((v == mx) & (a < best)));
         mx = b1 ? v : mx;
         best = b1 ? a : best;
-        const bool b2 = in && ((am >> a) & 1u) && (arg < 0 || v > amx || (v == amx && a < arg));
+        const bool b2 = in & (((am >> a) & 1u) != 0u) & ((arg < 0) | (v > amx) | ((v == amx) & (a < arg)));
         arg = b2 ? a : arg;
         amx = b2 ? v : amx;
       }
@@ -1114,7 +1119,7 @@ struct WEnv {
       rng.slo = rng_w[1];
       rng.ihi = rng_w[2];
       rng.ilo = rng_w[3];
-      rng.has = (uint32_t)(rng_w[4] >> 32);
+      rng.has = uni((uint32_t)(rng_w[4] >> 32));  // uniform: pcg_next32's branch on it stays scalar
       rng.buf = (uint32_t)rng_w[4];
       const uint32_t n = n_sw;
       const double eps = n < (uint32_t)EPS_WIN && n < (uint32_t)m.ntab ? unid(leps[n])
@@ -1187,6 +1192,9 @@ struct WEnv {
     d.row_cur = prr.row_base() + state;
     d.touch_cur = !explore;  // the key-set insert is done by post (one lane-0 region)
     if (!explore) action = ((amask >> best) & 1u) ? best : arg;
+    // the exploratory pick comes out of the vector-ALU generator: declare the action wave-uniform,
+    // so the apply below branches on the scalar unit instead of through exec-mask regions
+    action = uni(action);
     if (action < 0 || action >= na) lerr |= E_BAD_ACTION;
     SFL_LAP(7);
     SFL_PACC(1, t_eg);
