@@ -1136,8 +1136,8 @@ struct WEnv {
         bool slow = nvalid > 1u;
         if (slow && m.seedseq32) {
           const uint64_t mm = (uint64_t)ldc(m.seedseq32, (size_t)uni(sub_seed)) * nvalid;
-          const uint32_t thr = (0u - nvalid) % nvalid;
-          slow = (uint32_t)mm < thr;
+          // Lemire rejects when the low word is below (2^32 - n) % n < n: test against n first
+          slow = (uint32_t)mm < nvalid && (uint32_t)mm < (0u - nvalid) % nvalid;
           pick = (uint32_t)(mm >> 32);
         }
         if (slow) {
@@ -1145,9 +1145,11 @@ struct WEnv {
           pcg_from_seedseq(sub_seed, sub);
           pick = pcg_bounded(sub, nvalid - 1u);
         }
-        uint32_t mk = amask;
-        for (uint32_t kk = 0; kk < pick; ++kk) mk &= mk - 1u;
-        action = __builtin_ctz(mk);
+        // the pick-th allowed action: lane a holds action a, one ballot of its rank among the allowed
+        const uint32_t la16 = (uint32_t)lane & 15u;
+        const bool is_pick = lane < 16 && ((amask >> la16) & 1u) &&
+                             (uint32_t)__builtin_popcount(amask & ((1u << la16) - 1u)) == pick;
+        action = ctz64(__ballot(is_pick));
       }
       {  // uniform values, written by every lane
         lrng[0] = rng.shi;
@@ -1270,11 +1272,9 @@ struct WEnv {
     if (moving) {
       all_blocked = uni((uint32_t)blk_moving) != 0u;
     } else {
-      all_blocked = true;  // semaphores unchanged since the observation
-      for (int a = 0; a < na - 1; ++a) {
-        if (swr.src(a) != slot) continue;
-        if ((free_bits >> swr.dst(a)) & 1u) all_blocked = false;
-      }
+      // semaphores unchanged since the observation: no route from the in-port has a free out-port,
+      // i.e. the action mask holds STOP only
+      all_blocked = (amask & ((1u << (na - 1)) - 1u)) == 0u;
     }
     // reward_func.py:23-78: distance at the position projected along the non-STOP plan (staged
     // by prefetch for the STOP plan and for each final rail action of a route)
