@@ -90,7 +90,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--decisions", type=int, default=256, help="agent-env-steps per env per step (one launch)")
+    ap.add_argument("--decisions", type=int, default=1024, help="agent-env-steps per env per step (one launch)")
     ap.add_argument("--envs", type=int, default=65536, help="envs per GPU")
     ap.add_argument("--config", default="c3")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)

@@ -426,6 +426,137 @@ def generate(n_switches: int, n_trains: int, n_stations: int, seed: int, *,
     raise RuntimeError("could not generate a strongly connected scenario")
 
 
+# ---------------------------------------------------------------------------
+# Flatland-like city maps
+# ---------------------------------------------------------------------------
+
+def _straight(r0: int, c0: int, r1: int, c1: int, pairs: Dict[Tuple[int, int], Set[FrozenSet[int]]]) -> None:
+    """Plain track strictly between two cells of one row or column."""
+    if r0 == r1:
+        for c in range(min(c0, c1) + 1, max(c0, c1)):
+            pairs.setdefault((r0, c), set()).add(frozenset((E, W)))
+    else:
+        for r in range(min(r0, r1) + 1, max(r0, r1)):
+            pairs.setdefault((r, c0), set()).add(frozenset((N, S)))
+
+
+def city_network(n_lines: int, spacing: int, margin: int, cities: List[Tuple[int, int, int]],
+                 rng: np.random.Generator, slip_weights=(0.2, 0.3, 0.5)):
+    """A square backbone of ``n_lines`` x ``n_lines`` rail lines (the inter-city connections) with
+    cities on horizontal backbone segments, the way Flatland's sparse_rail_generator lays out a
+    city: ``P`` parallel tracks (the backbone line plus P-1 sidings two rows apart) between two
+    throats, each siding joining the main line through a T switch whose trunk faces out of the
+    city.  ``cities``: (row line i, column line j, tracks P) -- the city sits between column lines
+    j and j+1 on row line i.  Returns (grid, junction cells, per-city track cells, throat cells)."""
+    side_len = 2 * margin + (n_lines - 1) * spacing + 1
+    pos = [margin + k * spacing for k in range(n_lines)]
+    pairs: Dict[Tuple[int, int], Set[FrozenSet[int]]] = {}
+    for i in range(n_lines):
+        for j in range(n_lines - 1):
+            _straight(pos[i], pos[j], pos[i], pos[j + 1], pairs)
+            _straight(pos[j], pos[i], pos[j + 1], pos[i], pairs)
+    junctions = set()
+    for i in range(n_lines):
+        for j in range(n_lines):
+            sides = {d for d, ok in ((N, i > 0), (S, i < n_lines - 1), (W, j > 0), (E, j < n_lines - 1)) if ok}
+            pairs[(pos[i], pos[j])] = set(_junction_pairs(sides, rng, slip_weights))
+            if len(sides) >= 3:
+                junctions.add((pos[i], pos[j]))
+    city_tracks, throats = [], set()
+    for (i, j, P) in cities:
+        r0, cw, ce = pos[i], pos[j], pos[j + 1]
+        a, b = cw + 2 * P, ce - 2 * P  # the city's platform span on every track
+        if b - a < 6 or (i + 1 < n_lines and pos[i + 1] - r0 < 2 * P + 2) or (i + 1 >= n_lines and 2 * P > margin + 1):
+            raise ValueError("city does not fit its backbone segment")
+        tracks = [[(r0, c) for c in range(a + 1, b)]]
+        for k in range(1, P):
+            rk, xw, xe = r0 + 2 * k, a - (2 * k - 1), b + (2 * k - 1)
+            # throats: the main line's cell becomes a T (trunk out of the city)
+            pairs[(r0, xw)].add(frozenset((W, S)))
+            pairs[(r0, xe)].add(frozenset((E, S)))
+            junctions.update({(r0, xw), (r0, xe)})
+            throats.update({(r0, xw), (r0, xe)})
+            _straight(r0, xw, rk, xw, pairs)
+            _straight(r0, xe, rk, xe, pairs)
+            pairs.setdefault((rk, xw), set()).add(frozenset((N, E)))
+            pairs.setdefault((rk, xe), set()).add(frozenset((N, W)))
+            _straight(rk, xw, rk, xe, pairs)
+            tracks.append([(rk, c) for c in range(a + 1, b)])
+        city_tracks.append(tracks)
+    grid = np.zeros((side_len, side_len), dtype=np.int64)
+    for (r, c), prs in pairs.items():
+        grid[r, c] = pairs_to_bits(prs)
+    return grid, junctions, city_tracks, throats
+
+
+def generate_cities(n_cities: int, n_trains: int, seed: int, *, n_lines: Optional[int] = None, spacing: int = 20,
+                    margin: int = 7, tracks: Tuple[int, int] = (2, 3), malfunction: Tuple[float, int, int] = (0.0, 0, 0),
+                    name: str = "", slip_weights=(0.2, 0.3, 0.5), max_tries: int = 200) -> Scenario:
+    """Flatland-like scenario: ``n_cities`` cities of 2-3 parallel tracks with one station each on a
+    square backbone of inter-city lines; every train starts on a city track and targets the station
+    of another city; timetable as flatland_patch/timetable_generators.py (``timetable``)."""
+    if n_lines is None:
+        n_lines = 2
+        while n_lines * (n_lines - 1) < n_cities:
+            n_lines += 1
+    slots = [(i, j) for i in range(n_lines) for j in range(n_lines - 1)]
+    if n_cities > len(slots) or n_cities < 2:
+        raise ValueError("2 <= n_cities <= n_lines * (n_lines - 1)")
+    rng = np.random.default_rng(seed)
+    for _ in range(max_tries):
+        pick = sorted(int(x) for x in rng.choice(len(slots), size=n_cities, replace=False))
+        cities = [(slots[q][0], slots[q][1], int(rng.integers(tracks[0], tracks[1] + 1))) for q in pick]
+        grid, junctions, city_tracks, throats = city_network(n_lines, spacing, margin, cities, rng, slip_weights)
+        if not strongly_connected(grid):
+            continue
+        near_junction = lambda rc: any((rc[0] + dr, rc[1] + dc) in junctions for dr, dc in DELTA)  # noqa: E731
+        stations, pools = [], []
+        for tr in city_tracks:
+            t = tr[int(rng.integers(0, len(tr)))]
+            cells = t[len(t) // 3: 2 * len(t) // 3 + 1]
+            st = cells[int(rng.integers(0, len(cells)))]
+            stations.append(st)
+            pools.append([c for trk in tr for c in trk if c != st and not near_junction(c)])
+        dists = {st: distance_to_cell(grid, st) for st in stations}
+        trains: List[Train] = []
+        used = set()
+        for k in range(n_trains):
+            placed = False
+            for _try in range(100):
+                home = int(rng.integers(0, n_cities))
+                cand = [c for c in pools[home] if c not in used]
+                if not cand:
+                    continue
+                p0 = cand[int(rng.integers(0, len(cand)))]
+                h0 = (E, W)[int(rng.integers(0, 2))]
+                dest = int(rng.integers(0, n_cities - 1))
+                dest = dest + 1 if dest >= home else dest
+                tgt = stations[dest]
+                if tgt in _first_switch_chain(grid, junctions, p0, h0) or dists[tgt][p0[0], p0[1], h0] < 0:
+                    continue
+                used.add(p0)
+                trains.append(Train((int(p0[0]), int(p0[1])), int(h0), (int(tgt[0]), int(tgt[1]))))
+                placed = True
+                break
+            if not placed:
+                break
+        if len(trains) != n_trains:
+            continue
+        trains.sort(key=lambda t: (t.initial_position[0], t.initial_position[1], t.initial_direction))
+        lens = [int(dists[t.target][t.initial_position[0], t.initial_position[1], t.initial_direction]) + 1
+                for t in trains]
+        Hh, Ww = grid.shape
+        rs = np.random.RandomState(seed & 0x7FFFFFFF)
+        eds, las, mes = timetable(lens, Ww, Hh, n_cities, rs)
+        for t, ed, la in zip(trains, eds, las):
+            t.earliest_departure, t.latest_arrival = ed, la
+        return Scenario(height=Hh, width=Ww, grid=[[int(x) for x in row] for row in grid], trains=trains,
+                        max_episode_steps=int(mes), malfunction_rate=float(malfunction[0]),
+                        malfunction_min=int(malfunction[1]), malfunction_max=int(malfunction[2]),
+                        name=name, seed=int(seed))
+    raise RuntimeError("could not generate a strongly connected city scenario")
+
+
 # Named configurations (BASELINE.json configs; SURVEY.md §8(d) table)
 CONFIGS = {
     # C1: stands in for test_model.py's 18x18 / 5 cities / 2 trains map (Flatland's own map is unobtainable offline)
@@ -447,12 +578,21 @@ def from_flatland_params(width: int, height: int, max_num_cities: int, number_of
                          malfunction=(0.0, 0, 0), spacing: int = 5, margin: int = 3) -> Scenario:
     """Scenario for the reference's [ENV] config keys (main.py:21-60).
 
-    Flatland's sparse_rail_generator is absent, so the city layout is replaced by a line
-    grid of the same size: as many lines as fit in ``width`` x ``height``, one station per
-    city, ``number_of_agents`` trains."""
+    Flatland's sparse_rail_generator is absent; with two or more cities the map is a
+    ``generate_cities`` layout (cities of parallel tracks on a square backbone) at least
+    ``width`` x ``height``; with one city, a line grid of that size with one station."""
     size = max(int(width), int(height))
+    n_cities, n_agents = int(max_num_cities), int(number_of_agents)
+    if n_cities >= 2:
+        n_lines = 2
+        while n_lines * (n_lines - 1) < n_cities:
+            n_lines += 1
+        c_margin = 7
+        c_spacing = max(18, -(-(size - 2 * c_margin - 1) // (n_lines - 1)))
+        return generate_cities(n_cities, n_agents, seed=int(seed), n_lines=n_lines, spacing=c_spacing,
+                               margin=c_margin, malfunction=malfunction, name=f"flatland_{width}x{height}")
     n_lines = max(3, (size - 2 * margin - 1) // spacing + 1)
     n_sw = n_lines * n_lines - 4
-    return generate(n_switches=n_sw, n_trains=int(number_of_agents), n_stations=max(1, int(max_num_cities)),
-                    seed=int(seed), nx_lines=n_lines, ny_lines=n_lines, spacing=spacing, margin=margin,
-                    size=size, malfunction=malfunction, name=f"flatland_{width}x{height}")
+    return generate(n_switches=n_sw, n_trains=n_agents, n_stations=1, seed=int(seed), nx_lines=n_lines,
+                    ny_lines=n_lines, spacing=spacing, margin=margin, size=size, malfunction=malfunction,
+                    name=f"flatland_{width}x{height}")

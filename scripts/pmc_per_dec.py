@@ -7,7 +7,7 @@ import statistics
 import sys
 
 src = sys.argv[1]
-dec = float(sys.argv[2]) if len(sys.argv) > 2 else 65536 * 256  # bench.py default launch: 65,536 envs x 256 decisions
+dec = float(sys.argv[2]) if len(sys.argv) > 2 else 65536 * 1024  # bench.py default launch: 65,536 envs x 1024 decisions
 vals = {}
 for f in glob.glob(os.path.join(src, "*counter_collection.csv")) + glob.glob(os.path.join(src, "*", "*counter_collection.csv")):
     for r in csv.DictReader(open(f)):

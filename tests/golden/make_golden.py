@@ -161,6 +161,9 @@ CASES = [
     ("c2_mf", "c2", mapgen.MAP_SEED, (0.01, 5, 15), 450565, HP_TEST_MODEL, 20, None),
     ("c2_s3", "c2", 3, (0.03, 3, 9), 99, HP_DECAY, 15, 5),
     ("c3_mf", "c3", mapgen.MAP_SEED, (0.01, 5, 15), 450565, HP_TEST_MODEL, 3, None),
+    # Flatland-like city maps (mapgen.generate_cities: parallel city tracks, T-switch throats)
+    ("city4_mf", ("cities", 4, 6), mapgen.MAP_SEED, (0.01, 5, 15), 450565, HP_TEST_MODEL, 25, None),
+    ("city6_s5", ("cities", 6, 12), 5, (0.02, 3, 8), 2024, HP_DECAY, 10, 3),
 ]
 
 
@@ -169,7 +172,10 @@ def main(only=None):
     for name, cfg, mseed, mf, seed, hp, neps, exploit in CASES:
         if only and name not in only:
             continue
-        sc = mapgen.make_config(cfg, seed=mseed, malfunction=mf)
+        if isinstance(cfg, str):
+            sc = mapgen.make_config(cfg, seed=mseed, malfunction=mf)
+        else:
+            sc = mapgen.generate_cities(cfg[1], cfg[2], seed=mseed, malfunction=mf, name=name)
         data = run_case(name, sc, seed, hp, neps, exploit_freq=exploit)
         path = os.path.join(HERE, f"{name}.json.gz")
         with gzip.open(path, "wt") as f:
