@@ -70,9 +70,19 @@ def cpu_cxx_baseline(cm, seconds: float):
                        f"{n} decisions in {dt:.1f} s after one untimed 64-decision step")
 
 
-def pmc_traffic():
+def dist_setup(par, local: int):
+    """torch.distributed for the bench: RCCL ("nccl") over the GPUs of the node, one per rank.
+    SFL_DIST_BACKEND=gloo and SFL_DEVICE=<index> rehearse the multi-rank path with several ranks
+    on one GPU (the launcher, sharding and reductions; not the RCCL transport)."""
+    backend = os.environ.get("SFL_DIST_BACKEND", "nccl")
+    dev = int(os.environ.get("SFL_DEVICE", local))
+    dist = par.init(backend) if backend != "nccl" else par.init("nccl")
+    return dist, dev, ("cuda" if backend == "nccl" else "cpu")
+
+
+def pmc_traffic(workload: str):
     """HBM bytes per env-kernel launch from the committed rocprofv3 PMC summary of this exact kernel source
-    (profiles/*_pmc.json written by scripts/pmc_summary.py), or None."""
+    and workload (profiles/*_pmc.json written by scripts/pmc_summary.py), or None."""
     import glob
     sha = importlib.import_module(PKG + ".build").kernel_source_sha1()
     for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc.json")), reverse=True):
@@ -80,7 +90,7 @@ def pmc_traffic():
             d = json.load(open(f))
         except Exception:
             continue
-        if d.get("source_sha1") == sha:
+        if d.get("source_sha1") == sha and d.get("workload") == workload:
             return d["traffic_bytes_per_launch"], os.path.relpath(f, REPO)
     return None, None
 
@@ -105,8 +115,8 @@ def main():
     import torch
     par = importlib.import_module(PKG + ".parallel")
     world, rank, local = par.world()
-    dist = par.init("nccl")
-    torch.cuda.set_device(local)
+    dist, dev, red_dev = dist_setup(par, local)
+    torch.cuda.set_device(dev)
 
     mapgen = importlib.import_module(PKG + ".mapgen")
     comp = importlib.import_module(PKG + ".compiler")
@@ -115,7 +125,7 @@ def main():
     cm = comp.compile_scenario(sc)
     E = args.envs
     seeds = par.shard_seeds(450565, E, rank)
-    b = runtime.Batch(cm, HP, seeds, device=local)
+    b = runtime.Batch(cm, HP, seeds, device=dev)
     b.learn_begin()
     b.apply_qinit()
     for _ in range(args.warmup):
@@ -145,12 +155,14 @@ def main():
         ticks_l += cl["last_launch_ticks"]
     barrier()
     dt = time.perf_counter() - t0
-    dt, total_all = par.reduce_timing(dist, dt, float(total), device="cuda")
+    dt, total_all = par.reduce_timing(dist, dt, float(total), device=red_dev)
     if rank == 0:
         avg_ms = kms / max(1, args.steps)
         bytes_per_launch = abytes / max(1, args.steps)
         achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
-        traffic, traffic_src = pmc_traffic()
+        workload = (f"{args.config}: {cm.S} switches / {cm.T} trains, {E} envs per GPU, learning "
+                    f"(eps-greedy + Q update), {args.decisions} agent-env-steps per env per step")
+        traffic, traffic_src = pmc_traffic(workload)
         res = {
             "metric": METRIC,
             "value": total_all / dt,
@@ -165,8 +177,7 @@ def main():
             "dtype": "f64",
             "data": "synthetic 64-switch/32-train Flatland-format map (mapgen c3, seed 450565), random-init "
                     "(default_q + optimistic init) Q-tables",
-            "config": {"workload": f"{args.config}: {cm.S} switches / {cm.T} trains, {E} envs per GPU, learning "
-                                   f"(eps-greedy + Q update), {args.decisions} agent-env-steps per env per step",
+            "config": {"workload": workload,
                        "envs_per_gpu": E, "decisions_per_env_per_step": args.decisions,
                        "parallelism": f"env-batch dp{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -192,15 +203,15 @@ def bench_partition(args):
     par = importlib.import_module(PKG + ".parallel")
     part = importlib.import_module(PKG + ".partition")
     world, rank, local = par.world()
-    dist = par.init("nccl")
-    torch.cuda.set_device(local)
+    dist, dev, red_dev = dist_setup(par, local)
+    torch.cuda.set_device(dev)
     mapgen = importlib.import_module(PKG + ".mapgen")
     comp = importlib.import_module(PKG + ".compiler")
     cfg = args.config if args.config != "c3" else "c5"
     E = args.envs if args.envs != 65536 else 8192
     cm = comp.compile_scenario(mapgen.make_config(cfg))
     seeds = par.shard_seeds(450565, E, rank)
-    pb = part.PartitionedBatch(cm, HP, seeds, rank * E, world * E, rank=rank, world=world, dist=dist, device=local,
+    pb = part.PartitionedBatch(cm, HP, seeds, rank * E, world * E, rank=rank, world=world, dist=dist, device=dev,
                                buffer_device="cuda")
     pb.learn_begin()
     pb.apply_qinit()
@@ -220,7 +231,7 @@ def bench_partition(args):
     barrier()
     dt = time.perf_counter() - t0
     total = float(E * args.decisions * args.steps)
-    dt, total_all = par.reduce_timing(dist, dt, total, device="cuda")
+    dt, total_all = par.reduce_timing(dist, dt, total, device=red_dev)
     if rank == 0:
         res = {
             "metric": METRIC,

@@ -119,6 +119,11 @@ class PartitionedBatch:
     def _exchange(self, recv, send):
         if self.dist is None or self.world == 1:
             recv.copy_(send)
+        elif recv.is_cuda and self.dist.get_backend() == "gloo":
+            # gloo (multi-rank rehearsal on one GPU): exchange through host memory
+            r = self.torch.empty_like(recv, device="cpu")
+            self.dist.all_to_all_single(r, send.cpu())
+            recv.copy_(r)
         else:
             self.dist.all_to_all_single(recv, send)
         if self.on_gpu:

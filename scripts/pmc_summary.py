@@ -3,7 +3,9 @@
 FETCH_SIZE / WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE counts 64 B per 128-B request, i.e. half the
 bytes of a wide coalesced stream (MI355X_MICROARCH.md §HBM) — we apply that x2 correction and note
 that other access widths are uncalibrated.
-Usage: python scripts/pmc_summary.py gpurun_out/<tag> profiles/<name>.json
+Usage: python scripts/pmc_summary.py gpurun_out/<tag> profiles/<name>.json [bench.json of the same workload]
+The PMC passes run bench.py with its default workload; the bench line's config.workload is
+recorded so that bench.py reports the traffic only for that workload.
 """
 import csv
 import glob
@@ -14,7 +16,7 @@ import statistics
 import sys
 
 
-def main(src, dst):
+def main(src, dst, bench_json=None):
     vals = {}
     kname = None
     for d in sorted(glob.glob(os.path.join(src, "pmc_*"))):
@@ -36,9 +38,11 @@ def main(src, dst):
         out["l2_hit_rate"] = med["TCC_HIT_sum"] / max(1.0, med["TCC_HIT_sum"] + med["TCC_MISS_sum"])
     if "SQ_WAVE_CYCLES" in med:
         out["wait_fraction"] = med.get("SQ_WAIT_ANY", 0) / med["SQ_WAVE_CYCLES"]
+    if bench_json:
+        out["workload"] = json.load(open(bench_json))["config"]["workload"]
     json.dump(out, open(dst, "w"), indent=1)
     print(json.dumps(out, indent=1))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2])
+    main(*sys.argv[1:4])
