@@ -35,7 +35,7 @@ __global__ void __launch_bounds__(256) k_run(const sfl::SflMap* __restrict__ m, 
 // One env per wavefront (sfl_wave.h): 4 envs per block.  PPL / SPL = semaphore / counter
 // registers per lane (sfl::kVariants).
 template <int PPL, int SPL, int TW, bool TRACE>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SFL_WAVE_OCC))) k_wave(const sfl::SflMap* __restrict__ m, const sfl::SflState* __restrict__ s,
+__global__ void __launch_bounds__(SFL_WAVE_BLOCK) __attribute__((amdgpu_waves_per_eu(SFL_WAVE_OCC))) k_wave(const sfl::SflMap* __restrict__ m, const sfl::SflState* __restrict__ s,
                                               const sfl::SflCtl* __restrict__ c) {
   sfl::wave::run<PPL, SPL, TW, TRACE>(*m, *s, *c);
 }
@@ -227,10 +227,10 @@ struct HipBackend {
     const auto* pm = (const sfl::SflMap*)(base);
     const auto* ps = (const sfl::SflState*)(base + os);
     const auto* pc = (const sfl::SflCtl*)(base + oc);
-    const unsigned wblocks = (unsigned)(((size_t)s.E * 64 + 255) / 256);
+    const unsigned wblocks = (unsigned)(((size_t)s.E * 64 + SFL_WAVE_BLOCK - 1) / SFL_WAVE_BLOCK);
 #define SFL_KW(v)                                                                                                   \
-  (c.trace ? k_wave<sfl::kVariants[v].PPL, sfl::kVariants[v].SPL, sfl::kVariants[v].TW, true><<<wblocks, 256, 0, stream>>>(pm, ps, pc) \
-           : k_wave<sfl::kVariants[v].PPL, sfl::kVariants[v].SPL, sfl::kVariants[v].TW, false><<<wblocks, 256, 0, stream>>>(pm, ps, pc))
+  (c.trace ? k_wave<sfl::kVariants[v].PPL, sfl::kVariants[v].SPL, sfl::kVariants[v].TW, true><<<wblocks, SFL_WAVE_BLOCK, 0, stream>>>(pm, ps, pc) \
+           : k_wave<sfl::kVariants[v].PPL, sfl::kVariants[v].SPL, sfl::kVariants[v].TW, false><<<wblocks, SFL_WAVE_BLOCK, 0, stream>>>(pm, ps, pc))
     if (variant == 1) SFL_KW(1);
     else if (variant == 2) SFL_KW(2);
     else if (variant == 3) SFL_KW(3);

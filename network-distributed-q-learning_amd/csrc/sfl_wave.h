@@ -50,10 +50,9 @@ constexpr uint32_t PF_NONE = 0xFFFFFFFFu;
 // projected cell if it stops (reward of STOP), if it moves with final rail action 0..3 (reward of
 // a route), and the row's argmax | first allowed argmax << 8 under the staged observation
 constexpr int PF_W = 12, PF_I = 14;
-#ifndef SFL_EPS_WIN
-#define SFL_EPS_WIN 512
+#ifndef SFL_WAVE_BLOCK
+#define SFL_WAVE_BLOCK 256  // threads per k_wave block (envs per block x 64)
 #endif
-constexpr int EPS_WIN = SFL_EPS_WIN;  // epsilon table entries kept in LDS
 constexpr int32_t PF_OFFGRID = (int32_t)0x80000000;  // projection left the grid
 
 #define SFL_AS_G __attribute__((address_space(1)))
@@ -187,7 +186,6 @@ struct WEnv {
   uint32_t pf_roff;  // offset of the staged row in the env's Q block (PF_NONE: none)
   uint32_t pf_qoff;  // offset of the staged pending cell (PF_NONE: none)
   bool pf_ok;        // uniform: this batch has been prefetched
-  const double* leps;  // LDS copy of eps_tab[0, EPS_WIN) (shared by the block)
   uint32_t lerr;  // error bits seen by this lane (OR-reduced on store)
   // this env's blocks: Q-table, key-set bitmap, (switch, train) slots (env-major [T][S] here,
   // so one env's slots are contiguous and a flush over switches is one coalesced access)
@@ -211,8 +209,8 @@ struct WEnv {
   uint64_t lap_t = 0;
 #endif
 
-  __device__ WEnv(const SflMap& m_, const SflState& s_, uint32_t e_, int lane_, uint32_t* lds, const double* leps_)
-      : m(m_), s(s_), e(e_), E(s_.E), lane(lane_), mine(lane_ < m_.T), lsem(lds), lcnt(lds + 64 * PPL), lpf((double*)(lds + 64 * (PPL + SPL))), leps(leps_) {
+  __device__ WEnv(const SflMap& m_, const SflState& s_, uint32_t e_, int lane_, uint32_t* lds)
+      : m(m_), s(s_), e(e_), E(s_.E), lane(lane_), mine(lane_ < m_.T), lsem(lds), lcnt(lds + 64 * PPL), lpf((double*)(lds + 64 * (PPL + SPL))) {
     lrng = (uint64_t*)(lds + 64 * (PPL + SPL) + TWc * PF_W * 2);
     ltt = (const int32_t*)(lds + 64 * (PPL + SPL) + TWc * PF_W * 2 + 12);
     qb = s.q + (size_t)e * m.q_per_env;
@@ -1122,9 +1120,8 @@ struct WEnv {
       rng.has = uni((uint32_t)(rng_w[4] >> 32));  // uniform: pcg_next32's branch on it stays scalar
       rng.buf = (uint32_t)rng_w[4];
       const uint32_t n = n_sw;
-      const double eps = n < (uint32_t)EPS_WIN && n < (uint32_t)m.ntab ? unid(leps[n])
-                         : n < (uint32_t)m.ntab                      ? ldc(m.eps_tab, (size_t)n)
-                                                                     : m.eps0 * pow_ool(m.eps_decay, (double)n);
+      // eps0 * decay**n (distr_q.py:59-68): host-computed table (a scalar load, K$-resident), pow beyond it
+      const double eps = n < (uint32_t)m.ntab ? ldc(m.eps_tab, (size_t)n) : m.eps0 * pow_ool(m.eps_decay, (double)n);
       if (unid(pcg_double(rng)) < eps) {
         explore = true;
         const uint32_t sub_seed = pcg_bounded(rng, 2147483646u);
@@ -1396,12 +1393,9 @@ __device__ void run(const SflMap& m, const SflState& s, const SflCtl& c) {
   constexpr int LDS_WORDS = 64 * (PPL + SPL) + TW * PF_W * 2 + 12 + TW * 8;  // semaphores, counters, prefetch records, rng, timetable
   const int lane = (int)__lane_id();
   const uint32_t e = uni((uint32_t)((blockIdx.x * blockDim.x + threadIdx.x) >> 6));
-  __shared__ double leps[EPS_WIN];
-  for (int i = (int)threadIdx.x; i < EPS_WIN; i += (int)blockDim.x) leps[i] = i < m.ntab ? m.eps_tab[i] : 0.0;
-  __syncthreads();
   if (e >= s.E) return;
-  __shared__ uint32_t lds[4 * LDS_WORDS];
-  V v(m, s, e, lane, lds + (threadIdx.x >> 6) * LDS_WORDS, leps);
+  __shared__ uint32_t lds[(SFL_WAVE_BLOCK / 64) * LDS_WORDS];
+  V v(m, s, e, lane, lds + (threadIdx.x >> 6) * LDS_WORDS);
   v.load();
   int32_t phase = uni(ld(s.phase, e));
   int32_t ep_t = uni(ld(s.ep_t, e)), n_test = uni(ld(s.n_test, e));
