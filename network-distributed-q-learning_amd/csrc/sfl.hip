@@ -39,6 +39,14 @@ __global__ void __launch_bounds__(SFL_WAVE_BLOCK) __attribute__((amdgpu_waves_pe
                                               const sfl::SflCtl* __restrict__ c) {
   sfl::wave::run<PPL, SPL, TW, TRACE>(*m, *s, *c);
 }
+// maps with 65-128 trains (two train slots per lane): one env per 64-thread block (its LDS is
+// ~22 KB), register budget for the LDS-bound occupancy of 2 waves per SIMD
+template <int PPL, int SPL, int TW, bool TRACE>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_wave2(const sfl::SflMap* __restrict__ m,
+                                                                                   const sfl::SflState* __restrict__ s,
+                                                                                   const sfl::SflCtl* __restrict__ c) {
+  sfl::wave::run<PPL, SPL, TW, TRACE>(*m, *s, *c);
+}
 
 // graph-partitioned rounds (sfl_part.h): local env step (lane per env), segment headers,
 // owner-side answer and update (one thread per record)
@@ -231,10 +239,16 @@ struct HipBackend {
 #define SFL_KW(v)                                                                                                   \
   (c.trace ? k_wave<sfl::kVariants[v].PPL, sfl::kVariants[v].SPL, sfl::kVariants[v].TW, true><<<wblocks, SFL_WAVE_BLOCK, 0, stream>>>(pm, ps, pc) \
            : k_wave<sfl::kVariants[v].PPL, sfl::kVariants[v].SPL, sfl::kVariants[v].TW, false><<<wblocks, SFL_WAVE_BLOCK, 0, stream>>>(pm, ps, pc))
+#define SFL_KW2(v)                                                                                       \
+  (c.trace ? k_wave2<sfl::kVariants[v].PPL, sfl::kVariants[v].SPL, sfl::kVariants[v].TW, true><<<s.E, 64, 0, stream>>>(pm, ps, pc) \
+           : k_wave2<sfl::kVariants[v].PPL, sfl::kVariants[v].SPL, sfl::kVariants[v].TW, false><<<s.E, 64, 0, stream>>>(pm, ps, pc))
+    static_assert(sfl::kVariants[5].TW > 64 && sfl::kNumVariants == 6, "variant 5 is the two-slot shape");
     if (variant == 1) SFL_KW(1);
     else if (variant == 2) SFL_KW(2);
     else if (variant == 3) SFL_KW(3);
     else if (variant == 4) SFL_KW(4);
+    else if (variant == 5) SFL_KW2(5);
+#undef SFL_KW2
 #undef SFL_KW
     else if (m.T <= 32) k_run<1><<<blocks, 256, 0, stream>>>(pm, ps, pc);
     else if (m.T <= 64) k_run<2><<<blocks, 256, 0, stream>>>(pm, ps, pc);

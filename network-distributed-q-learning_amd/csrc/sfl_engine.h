@@ -86,17 +86,17 @@ struct Handle {
 struct WaveShape {
   int PPL, SPL, TW;
 };
-constexpr WaveShape kVariants[] = {{0, 0, 0}, {1, 1, 32}, {4, 1, 32}, {4, 1, 64}, {8, 2, 64}};
-constexpr int kNumVariants = 5;
+constexpr WaveShape kVariants[] = {{0, 0, 0}, {1, 1, 32}, {4, 1, 32}, {4, 1, 64}, {8, 2, 64}, {16, 4, 128}};
+constexpr int kNumVariants = 6;
 
-// Eligibility: trains fit one lane each (T <= 64, 64-bit masks), the env fits the variant's
+// Eligibility: trains fit one or two slots per lane (T <= 128), the env fits the variant's
 // registers and every semaphore time fits the 11-bit register field.  SFL_KERNEL=scalar
 // forces k_run.
 inline int choose_variant(const sfl_map_desc* md, bool backend_has_wave) {
   if (!backend_has_wave) return 0;
   const char* env = getenv("SFL_KERNEL");
   if (env && strcmp(env, "scalar") == 0) return 0;
-  if (md->T > 64) return 0;
+  if (md->T > 128) return 0;
   int32_t ed_max = 0, ed_min = 0, dist_max = 0, len_max = 0;
   for (int32_t h = 0; h < md->T; ++h) {
     ed_max = md->tr_ed[h] > ed_max ? md->tr_ed[h] : ed_max;

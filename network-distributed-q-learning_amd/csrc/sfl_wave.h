@@ -121,6 +121,59 @@ __device__ __attribute__((noinline)) double pow_ool(double base, double n) { ret
 __device__ __forceinline__ int ctz64(uint64_t x) { return __builtin_ctzll(x); }
 __device__ __forceinline__ int popc64(uint64_t x) { return __builtin_popcountll(x); }
 
+// Train masks.  A map with up to 64 trains keeps one train per lane and 64-bit masks; up to 128
+// trains, lane l holds trains l and l + 64 (TPL = 2 "train slots" per lane) and a mask is two
+// words.  The helpers below are overloaded on both, so the TPL = 1 code is the plain uint64_t code.
+struct M2 {
+  uint64_t w[2];
+};
+__device__ __forceinline__ M2 operator|(M2 a, M2 b) { return M2{{a.w[0] | b.w[0], a.w[1] | b.w[1]}}; }
+__device__ __forceinline__ M2 operator&(M2 a, M2 b) { return M2{{a.w[0] & b.w[0], a.w[1] & b.w[1]}}; }
+__device__ __forceinline__ M2 operator~(M2 a) { return M2{{~a.w[0], ~a.w[1]}}; }
+__device__ __forceinline__ M2& operator|=(M2& a, M2 b) { return a = a | b; }
+__device__ __forceinline__ M2& operator&=(M2& a, M2 b) { return a = a & b; }
+__device__ __forceinline__ bool operator==(M2 a, M2 b) { return a.w[0] == b.w[0] && a.w[1] == b.w[1]; }
+__device__ __forceinline__ bool many(uint64_t m) { return m != 0ull; }
+__device__ __forceinline__ bool many(M2 m) { return (m.w[0] | m.w[1]) != 0ull; }
+__device__ __forceinline__ int mctz(uint64_t m) { return ctz64(m); }
+__device__ __forceinline__ int mctz(M2 m) { return m.w[0] ? ctz64(m.w[0]) : 64 + ctz64(m.w[1]); }
+__device__ __forceinline__ void mclear_low(uint64_t& m) { m &= m - 1ull; }
+__device__ __forceinline__ void mclear_low(M2& m) {
+  if (m.w[0]) m.w[0] &= m.w[0] - 1ull;
+  else m.w[1] &= m.w[1] - 1ull;
+}
+__device__ __forceinline__ int mpopc(uint64_t m) { return popc64(m); }
+__device__ __forceinline__ int mpopc(M2 m) { return popc64(m.w[0]) + popc64(m.w[1]); }
+__device__ __forceinline__ bool mbit(uint64_t m, int i) { return ((m >> i) & 1ull) != 0ull; }
+__device__ __forceinline__ bool mbit(M2 m, int i) { return (((i & 64) ? m.w[1] : m.w[0]) >> (i & 63)) & 1ull; }
+__device__ __forceinline__ uint64_t mone(uint64_t, int i) { return 1ull << i; }
+__device__ __forceinline__ M2 mone(M2, int i) { return (i & 64) ? M2{{0ull, 1ull << (i & 63)}} : M2{{1ull << i, 0ull}}; }
+// bits below i (i < 64 for one word, < 128 for two)
+__device__ __forceinline__ uint64_t mbelow(uint64_t, int i) { return (1ull << i) - 1ull; }
+__device__ __forceinline__ M2 mbelow(M2, int i) {
+  return (i & 64) ? M2{{~0ull, (1ull << (i & 63)) - 1ull}} : M2{{(1ull << i) - 1ull, 0ull}};
+}
+__device__ __forceinline__ int mhighest(uint64_t m) { return 63 - __builtin_clzll(m); }
+__device__ __forceinline__ int mhighest(M2 m) { return m.w[1] ? 127 - __builtin_clzll(m.w[1]) : 63 - __builtin_clzll(m.w[0]); }
+__device__ __forceinline__ uint64_t mfirst(uint64_t, int n) { return n >= 64 ? ~0ull : (1ull << n) - 1ull; }
+__device__ __forceinline__ M2 mfirst(M2, int n) {
+  return n >= 128 ? M2{{~0ull, ~0ull}} : n >= 64 ? M2{{~0ull, (n == 64) ? 0ull : (1ull << (n - 64)) - 1ull}} : M2{{(1ull << n) - 1ull, 0ull}};
+}
+template <int TPL>
+struct MaskOf {
+  using type = uint64_t;
+};
+template <>
+struct MaskOf<2> {
+  using type = M2;
+};
+// one ballot per train slot
+template <int TPL>
+__device__ __forceinline__ typename MaskOf<TPL>::type mballot(const bool (&p)[TPL]) {
+  if constexpr (TPL == 1) return __ballot(p[0]);
+  else return M2{{__ballot(p[0]), __ballot(p[1])}};
+}
+
 // max over each quad of lanes (DPP quad permutes; the result is valid in every lane of the quad)
 template <int CTRL>
 __device__ __forceinline__ double dpp_f64(double x) {
@@ -165,13 +218,15 @@ struct WEnv {
   const SflState& s;
   const uint32_t e, E;
   const int lane;
-  const bool mine;  // lane < T: this lane holds train `lane`
-  // train `lane`
-  int32_t pos;
-  uint32_t bits, plan;
-  uint32_t nprv;  // next port | prev port << 16
-  uint32_t sdec;  // source port | decision switch << 16
-  int32_t delay;
+  static constexpr int TPL = (TWc + 63) / 64;  // train slots per lane: trains lane, lane + 64
+  using Mask = typename MaskOf<TPL>::type;
+  bool mine[TPL];  // lane + 64 k < T: slot k holds train lane + 64 k
+  // the lane's trains (slot k = train lane + 64 k)
+  int32_t pos[TPL];
+  uint32_t bits[TPL], plan[TPL];
+  uint32_t nprv[TPL];  // next port | prev port << 16
+  uint32_t sdec[TPL];  // source port | decision switch << 16
+  int32_t delay[TPL];
   // timetable constants of train `lane` (tr_pack)
   // timetable constants of the lane's train (tr_pack row) live in LDS and are read where used
   const int32_t* ltt;  // [TW][8]
@@ -183,8 +238,8 @@ struct WEnv {
   // batch prefetch (see prefetch()): per queued train (lane), the staged Q row, the pending
   // update's Q cell value and the slot word in LDS, and the staged offsets in VGPRs
   double* lpf;       // [64][PF_W]: row columns 0-3 | pending cell value | slot word (as bits) | int32 distances (PF_D0..)
-  uint32_t pf_roff;  // offset of the staged row in the env's Q block (PF_NONE: none)
-  uint32_t pf_qoff;  // offset of the staged pending cell (PF_NONE: none)
+  uint32_t pf_roff[TPL];  // offset of the staged row in the env's Q block (PF_NONE: none)
+  uint32_t pf_qoff[TPL];  // offset of the staged pending cell (PF_NONE: none)
   bool pf_ok;        // uniform: this batch has been prefetched
   uint32_t lerr;  // error bits seen by this lane (OR-reduced on store)
   // this env's blocks: Q-table, key-set bitmap, (switch, train) slots (env-major [T][S] here,
@@ -195,7 +250,7 @@ struct WEnv {
   // wave-uniform env scalars
   int32_t now;
   uint32_t flags, epoch;
-  uint64_t q_mask, arr_mask, fl_mask, mf_mask;
+  Mask q_mask, arr_mask, fl_mask, mf_mask;
   // the epsilon-greedy stream (numpy PCG64 state, increment, buffered half) lives in LDS: it is
   // touched once per decision and would otherwise hold ten registers across the whole loop
   uint64_t* lrng;  // [6]: state hi, lo, inc hi, lo, has << 32 | buf
@@ -210,12 +265,16 @@ struct WEnv {
 #endif
 
   __device__ WEnv(const SflMap& m_, const SflState& s_, uint32_t e_, int lane_, uint32_t* lds)
-      : m(m_), s(s_), e(e_), E(s_.E), lane(lane_), mine(lane_ < m_.T), lsem(lds), lcnt(lds + 64 * PPL), lpf((double*)(lds + 64 * (PPL + SPL))) {
+      : m(m_), s(s_), e(e_), E(s_.E), lane(lane_), lsem(lds), lcnt(lds + 64 * PPL), lpf((double*)(lds + 64 * (PPL + SPL))) {
+#pragma unroll
+    for (int k = 0; k < TPL; ++k) {
+      mine[k] = lane_ + 64 * k < m_.T;
+      pf_roff[k] = pf_qoff[k] = PF_NONE;
+    }
     lrng = (uint64_t*)(lds + 64 * (PPL + SPL) + TWc * PF_W * 2);
     ltt = (const int32_t*)(lds + 64 * (PPL + SPL) + TWc * PF_W * 2 + 12);
     qb = s.q + (size_t)e * m.q_per_env;
     pf_ok = false;
-    pf_roff = pf_qoff = PF_NONE;
     touchb = s.touched + (size_t)e * m.touched_words;
     slotb = s.slot + (size_t)e * (uint32_t)(m.S * m.T);
   }
@@ -234,11 +293,25 @@ struct WEnv {
     lcnt[sw] = v;  // wave-uniform value from every lane
   }
   __device__ __forceinline__ uint32_t cget_var(int sw) const { return lcnt[sw]; }  // per-lane index
+  // train h's value of a per-train register (h wave-uniform)
   template <class T>
-  __device__ __forceinline__ void tset(T& x, int h, T v) {
-    x = (lane == h) ? v : x;
+  __device__ __forceinline__ T trl(const T (&x)[TPL], int h) const {
+    if constexpr (TPL == 1) return rl(x[0], h);
+    else return rl((h & 64) ? x[1] : x[0], h & 63);
   }
-  __device__ __forceinline__ uint32_t state_of(int h) const { return tb_state(rl(bits, h)); }
+  template <class T>
+  __device__ __forceinline__ void tset(T (&x)[TPL], int h, T v) {
+#pragma unroll
+    for (int k = 0; k < TPL; ++k) x[k] = (lane + 64 * k == h) ? v : x[k];
+  }
+  __device__ __forceinline__ uint32_t state_of(int h) const { return tb_state(trl(bits, h)); }
+  // malfunctioning trains (check_port_blocked's owner test)
+  __device__ __forceinline__ Mask malf_mask() const {
+    bool p[TPL];
+#pragma unroll
+    for (int k = 0; k < TPL; ++k) p[k] = mine[k] && tb_state(bits[k]) == S_MALF;
+    return mballot<TPL>(p);
+  }
 
   // ---- map records --------------------------------------------------------------------
   __device__ __forceinline__ SwRec sw_rec(int sw) const { return SwRec{ldcv<u8>(m.sw_pack, (size_t)sw * 2u)}; }
@@ -314,57 +387,15 @@ struct WEnv {
 
   // ---- semaphores (wave-uniform) ----------------------------------------------------------
   // observer.py:44-151 (a record's dir field always equals map_direction(port))
-  __device__ __forceinline__ bool port_blocked(int next_p, int out_p, int h) const {
-    uint32_t r = sget(next_p);
-    if (r_present(r) && r_owner(r) != (uint32_t)h && r_t0(r) <= now && now <= r_t1(r)) {
-      if (!r_in(r)) return true;
-      if (state_of((int)r_owner(r)) == S_MALF) return true;
-    }
-    r = sget(out_p);
-    if (r_present(r) && r_owner(r) != (uint32_t)h && r_t0(r) <= now && now <= r_t1(r)) {
-      if (r_in(r)) return true;
-      if (state_of((int)r_owner(r)) == S_MALF) return true;
-    }
-    return false;
-  }
   // does record r block a train h entering through its port (io = 0: the next port) or leaving
   // through it (io = 1: the out port)?  0/1 in integer VALU: present, owned by another train,
   // inside its [t0, t1] window, and of the opposite direction or owned by a malfunctioning train
-  __device__ __forceinline__ uint32_t rec_blocks(uint32_t r, uint32_t h, uint64_t malf, uint32_t io) const {
+  __device__ __forceinline__ uint32_t rec_blocks(uint32_t r, uint32_t h, Mask malf, uint32_t io) const {
     const uint32_t ow = r_owner(r);
     const uint32_t win = (uint32_t)(~((now - r_t0(r)) | (r_t1(r) - now))) >> 31;
     const uint32_t other = ((ow ^ h) + 0xFFu) >> 8;
-    const uint32_t mf = (uint32_t)(malf >> ow) & 1u;
+    const uint32_t mf = mbit(malf, (int)ow) ? 1u : 0u;
     return (r >> 31) & win & other & ((r_in(r) ^ io ^ 1u) | mf);
-  }
-  // check_port_blocked for every record at once: lane-parallel over each lane's records, one
-  // ballot per register.  bn: the record blocks a train entering through it (next port),
-  // bo: it blocks a train leaving through it (out port).
-  struct Blocked {
-    uint64_t bn[PPL], bo[PPL];
-    __device__ __forceinline__ bool port(int next_p, int out_p) const {
-      uint64_t n = 0, o = 0;
-#pragma unroll
-      for (int k = 0; k < PPL; ++k) {
-        n = (k == (next_p >> 6)) ? bn[k] : n;
-        o = (k == (out_p >> 6)) ? bo[k] : o;
-      }
-      return (((n >> (next_p & 63)) | (o >> (out_p & 63))) & 1ull) != 0;
-    }
-  };
-  __device__ __forceinline__ Blocked blocked_masks(int h) const {
-    const uint64_t malf = __ballot(mine && tb_state(bits) == S_MALF);
-    Blocked bl;
-#pragma unroll
-    for (int k = 0; k < PPL; ++k) {
-      const uint32_t r = sem(k);
-      const uint32_t ow = r_owner(r);
-      const bool live = r_present(r) && ow != (uint32_t)h && r_t0(r) <= now && now <= r_t1(r);
-      const bool mf = (malf >> ow) & 1ull;
-      bl.bn[k] = __ballot(live && (!r_in(r) || mf));
-      bl.bo[k] = __ballot(live && (r_in(r) || mf));
-    }
-    return bl;
   }
   // put_keep / put_replace as value transforms of a record (vector ALU, wave-uniform values)
   struct PutF {
@@ -448,22 +479,26 @@ struct WEnv {
 
   // ---- launch-boundary state transfer ---------------------------------------------------------
   __device__ __forceinline__ void load() {
-    if (mine) {
-      pos = ld(s.tr_pos, ix(lane));
-      bits = ld(s.tr_bits, ix(lane));
-      plan = ld(s.tr_plan, ix(lane));
-      nprv = (uint32_t)ld(s.tr_next, ix(lane)) | ((uint32_t)ld(s.tr_prev, ix(lane)) << 16);
-      sdec = (uint32_t)ld(s.tr_src, ix(lane)) | ((uint32_t)ld(s.tr_dec, ix(lane)) << 16);
-      delay = ld(s.tr_delay, ix(lane));
-      *(vec_t<int32_t, 4>*)(ltt + 8 * lane) = ld((const vec_t<int32_t, 4>*)m.tr_pack, (size_t)lane * 2u);
-      *(vec_t<int32_t, 4>*)(ltt + 8 * lane + 4) = ld((const vec_t<int32_t, 4>*)m.tr_pack, (size_t)lane * 2u + 1u);
-    } else {
-      pos = -1;
-      bits = 0;
-      plan = 0;
-      nprv = 0xFFFFFFFFu;
-      sdec = 0xFFFFFFFFu;
-      delay = 0;
+#pragma unroll
+    for (int k = 0; k < TPL; ++k) {
+      const int hk = lane + 64 * k;
+      if (mine[k]) {
+        pos[k] = ld(s.tr_pos, ix(hk));
+        bits[k] = ld(s.tr_bits, ix(hk));
+        plan[k] = ld(s.tr_plan, ix(hk));
+        nprv[k] = (uint32_t)ld(s.tr_next, ix(hk)) | ((uint32_t)ld(s.tr_prev, ix(hk)) << 16);
+        sdec[k] = (uint32_t)ld(s.tr_src, ix(hk)) | ((uint32_t)ld(s.tr_dec, ix(hk)) << 16);
+        delay[k] = ld(s.tr_delay, ix(hk));
+        *(vec_t<int32_t, 4>*)(ltt + 8 * hk) = ld((const vec_t<int32_t, 4>*)m.tr_pack, (size_t)hk * 2u);
+        *(vec_t<int32_t, 4>*)(ltt + 8 * hk + 4) = ld((const vec_t<int32_t, 4>*)m.tr_pack, (size_t)hk * 2u + 1u);
+      } else {
+        pos[k] = -1;
+        bits[k] = 0;
+        plan[k] = 0;
+        nprv[k] = 0xFFFFFFFFu;
+        sdec[k] = 0xFFFFFFFFu;
+        delay[k] = 0;
+      }
     }
 #pragma unroll
     for (int k = 0; k < PPL; ++k) {
@@ -479,9 +514,13 @@ struct WEnv {
     flags = uni(ld(s.eflags, e));
     epoch = uni(ld(s.epoch, e));
     lerr = uni(ld(s.err, e));
-    auto mask = [&](int k) {
-      return uni((uint64_t)ld(s.masks, (size_t)(k * MAXW + 0) * E + e) |
-                 ((uint64_t)ld(s.masks, (size_t)(k * MAXW + 1) * E + e) << 32));
+    auto word = [&](int k, int w) {
+      return uni((uint64_t)ld(s.masks, (size_t)(k * MAXW + 2 * w) * E + e) |
+                 ((uint64_t)ld(s.masks, (size_t)(k * MAXW + 2 * w + 1) * E + e) << 32));
+    };
+    auto mask = [&](int k) -> Mask {
+      if constexpr (TPL == 1) return word(k, 0);
+      else return M2{{word(k, 0), word(k, 1)}};
     };
     q_mask = mask(0);
     arr_mask = mask(1);
@@ -496,15 +535,19 @@ struct WEnv {
     n_dec = 0;
   }
   __device__ __forceinline__ void store(int32_t phase) {
-    if (mine) {
-      st(s.tr_pos, ix(lane), pos);
-      st(s.tr_bits, ix(lane), bits);
-      st(s.tr_plan, ix(lane), plan);
-      st(s.tr_next, ix(lane), (uint16_t)(nprv & 0xFFFFu));
-      st(s.tr_prev, ix(lane), (uint16_t)(nprv >> 16));
-      st(s.tr_src, ix(lane), (uint16_t)(sdec & 0xFFFFu));
-      st(s.tr_dec, ix(lane), (uint16_t)(sdec >> 16));
-      st(s.tr_delay, ix(lane), delay);
+#pragma unroll
+    for (int k = 0; k < TPL; ++k) {
+      const int hk = lane + 64 * k;
+      if (mine[k]) {
+        st(s.tr_pos, ix(hk), pos[k]);
+        st(s.tr_bits, ix(hk), bits[k]);
+        st(s.tr_plan, ix(hk), plan[k]);
+        st(s.tr_next, ix(hk), (uint16_t)(nprv[k] & 0xFFFFu));
+        st(s.tr_prev, ix(hk), (uint16_t)(nprv[k] >> 16));
+        st(s.tr_src, ix(hk), (uint16_t)(sdec[k] & 0xFFFFu));
+        st(s.tr_dec, ix(hk), (uint16_t)(sdec[k] >> 16));
+        st(s.tr_delay, ix(hk), delay[k]);
+      }
     }
 #pragma unroll
     for (int k = 0; k < PPL; ++k) {
@@ -526,14 +569,22 @@ struct WEnv {
       st(s.eflags, e, flags);
       st(s.epoch, e, epoch);
       st(s.err, e, err);
-      st(s.masks, (size_t)(0 * MAXW + 0) * E + e, (uint32_t)q_mask);
-      st(s.masks, (size_t)(0 * MAXW + 1) * E + e, (uint32_t)(q_mask >> 32));
-      st(s.masks, (size_t)(1 * MAXW + 0) * E + e, (uint32_t)arr_mask);
-      st(s.masks, (size_t)(1 * MAXW + 1) * E + e, (uint32_t)(arr_mask >> 32));
-      st(s.masks, (size_t)(2 * MAXW + 0) * E + e, (uint32_t)fl_mask);
-      st(s.masks, (size_t)(2 * MAXW + 1) * E + e, (uint32_t)(fl_mask >> 32));
-      st(s.masks, (size_t)(3 * MAXW + 0) * E + e, (uint32_t)mf_mask);
-      st(s.masks, (size_t)(3 * MAXW + 1) * E + e, (uint32_t)(mf_mask >> 32));
+      auto put = [&](int k, const Mask& mk) {
+        uint64_t w[2];
+        if constexpr (TPL == 1) {
+          w[0] = mk;
+          w[1] = 0ull;
+        } else {
+          w[0] = mk.w[0];
+          w[1] = mk.w[1];
+        }
+#pragma unroll
+        for (int j = 0; j < 2 * TPL; ++j) st(s.masks, (size_t)(k * MAXW + j) * E + e, (uint32_t)(w[j >> 1] >> (32 * (j & 1))));
+      };
+      put(0, q_mask);
+      put(1, arr_mask);
+      put(2, fl_mask);
+      put(3, mf_mask);
       st(s.rng, ix(0), lrng[0]);
       st(s.rng, ix(1), lrng[1]);
       st(s.rng, ix(4), lrng[4]);
@@ -549,13 +600,17 @@ struct WEnv {
   // ---- episode reset (switch_env.py:93-158, _init_ports 507-568) --------------------------------
   __device__ __forceinline__ void reset() {
     now = 0;
-    if (mine) {
-      const uint32_t t_init = (uint32_t)ltt[8 * lane + 7];
-      pos = -1;
-      bits = tb_make(t_init & 0xFFu, S_WAITING, A_NONE, 0, 0, 0);
-      plan = 0;
-      nprv = (nprv & 0xFFFF0000u) | (t_init >> 16);
-      delay = ltt[8 * lane + 6];
+#pragma unroll
+    for (int k = 0; k < TPL; ++k) {
+      if (mine[k]) {
+        const int hk = lane + 64 * k;
+        const uint32_t t_init = (uint32_t)ltt[8 * hk + 7];
+        pos[k] = -1;
+        bits[k] = tb_make(t_init & 0xFFu, S_WAITING, A_NONE, 0, 0, 0);
+        plan[k] = 0;
+        nprv[k] = (nprv[k] & 0xFFFF0000u) | (t_init >> 16);
+        delay[k] = ltt[8 * hk + 6];
+      }
     }
 #pragma unroll
     for (int k = 0; k < PPL; ++k) sem(k) = 0u;
@@ -564,7 +619,7 @@ struct WEnv {
       sset((int)((uint32_t)tr[7] >> 16), r_pack(h, 1, tr[0] - 2, tr[0] + tr[5]));
     }
     flags &= ~(F_TERM | F_TRUNC | F_OWN_SCAN | F_INFLIGHT);
-    q_mask = arr_mask = fl_mask = mf_mask = 0;
+    q_mask = arr_mask = fl_mask = mf_mask = Mask{};
     // new (switch, train) epoch: slots from older episodes read as empty
     epoch = (epoch + 1u) & 0xFFu;
     if (epoch == 0) {
@@ -585,249 +640,315 @@ struct WEnv {
     pf_ok = false;
     const int32_t t = ++now;
     const uint64_t seed = s.seed[e];
-    const int h = lane;
-    const vec_t<int32_t, 4> tt0 = *(const vec_t<int32_t, 4>*)(ltt + 8 * (mine ? lane : 0));
-    const vec_t<int32_t, 4> tt1 = *(const vec_t<int32_t, 4>*)(ltt + 8 * (mine ? lane : 0) + 4);
-    const int32_t t_ed = tt0[0], t_target = tt0[3], t_init_cell = tt1[0];
-    const uint32_t t_init_dir = (uint32_t)tt1[3] & 0xFFu;
+    // the trains' timetable rows (LDS)
+    vec_t<int32_t, 4> tt0[TPL], tt1[TPL];
+#pragma unroll
+    for (int k = 0; k < TPL; ++k) {
+      tt0[k] = *(const vec_t<int32_t, 4>*)(ltt + 8 * (mine[k] ? lane + 64 * k : 0));
+      tt1[k] = *(const vec_t<int32_t, 4>*)(ltt + 8 * (mine[k] ? lane + 64 * k : 0) + 4);
+    }
     // pass 1: plan pop + prediction, malfunction draw, action preprocessing, desired move
-    bool mover = false;
-    int32_t desired = -1, pred = -1;
-    uint32_t aux = 0;
-    if (mine) {
-      const uint32_t b = bits;
-      const int32_t p0 = pos;
-      uint32_t st_ = tb_state(b), dir = tb_dir(b), prev = tb_prev(b), saved = tb_saved(b), mf = tb_mf(b);
-      uint32_t given = A_NOTHING;
-      pred = p0;
-      // every check_action of this pass is at (pc, pd): one 16-byte load of the move-table row
-      const int pc = p0 >= 0 ? p0 : t_init_cell;
-      const int pd = p0 >= 0 ? (int)dir : (int)t_init_dir;
-      const u4 mrow = ld((const u4*)m.move_tab, (size_t)((uint32_t)pc * 4u + (uint32_t)pd));
-      auto mv_of = [&](uint32_t a) -> Move {
-        const uint32_t k = a & 3u;
-        return unpack_move(k == 0 ? mrow[0] : k == 1 ? mrow[1] : k == 2 ? mrow[2] : mrow[3]);
-      };
-      if (!tb_done(b)) {
-        const uint32_t pl = plan;
-        if (pl_len(pl) == 0) {
-          given = A_FWD;
-        } else {
-          given = pl_front(pl);
-          prev = given;
-          plan = pl_pop(pl);
-        }
-        if (p0 >= 0) {
-          const Move mv = mv_of(given);
-          aux |= 1u << 12;
-          if (mv.valid) {
-            aux |= 1u << 13;
-            pred = mv.cell;
-            if (dest_sw(mv) >= 0) aux |= 1u << 14;  // the predicted cell is a switch cell
+    bool mover[TPL];
+    int32_t desired[TPL], pred[TPL];
+    uint32_t aux[TPL];
+#pragma unroll
+    for (int k = 0; k < TPL; ++k) {
+      const int h = lane + 64 * k;
+      const int32_t t_init_cell = tt1[k][0];
+      const uint32_t t_init_dir = (uint32_t)tt1[k][3] & 0xFFu;
+      mover[k] = false;
+      desired[k] = -1;
+      pred[k] = -1;
+      aux[k] = 0;
+      if (mine[k]) {
+        const uint32_t b = bits[k];
+        const int32_t p0 = pos[k];
+        uint32_t st_ = tb_state(b), dir = tb_dir(b), prev = tb_prev(b), saved = tb_saved(b), mf = tb_mf(b);
+        uint32_t given = A_NOTHING;
+        pred[k] = p0;
+        // every check_action of this pass is at (pc, pd): one 16-byte load of the move-table row
+        const int pc = p0 >= 0 ? p0 : t_init_cell;
+        const int pd = p0 >= 0 ? (int)dir : (int)t_init_dir;
+        const u4 mrow = ld((const u4*)m.move_tab, (size_t)((uint32_t)pc * 4u + (uint32_t)pd));
+        auto mv_of = [&](uint32_t a) -> Move {
+          const uint32_t q = a & 3u;
+          return unpack_move(q == 0 ? mrow[0] : q == 1 ? mrow[1] : q == 2 ? mrow[2] : mrow[3]);
+        };
+        if (!tb_done(b)) {
+          const uint32_t pl = plan[k];
+          if (pl_len(pl) == 0) {
+            given = A_FWD;
+          } else {
+            given = pl_front(pl);
+            prev = given;
+            plan[k] = pl_pop(pl);
+          }
+          if (p0 >= 0) {
+            const Move mv = mv_of(given);
+            aux[k] |= 1u << 12;
+            if (mv.valid) {
+              aux[k] |= 1u << 13;
+              pred[k] = mv.cell;
+              if (dest_sw(mv) >= 0) aux[k] |= 1u << 14;  // the predicted cell is a switch cell
+            }
           }
         }
+        if (st_ != S_DONE && mf == 0 && m.mf_rate > 0.0) {
+          const uint64_t z = mf_draw(seed, (uint64_t)t, (uint64_t)h);
+          const double u = (double)(z >> 11) * (1.0 / 9007199254740992.0);
+          if (u < m.mf_rate)
+            mf = (uint32_t)(m.mf_min + (int32_t)(mix64(z ^ 0xA0761D6478BD642Full) % (uint64_t)(m.mf_max - m.mf_min + 1))) + 1u;
+        }
+        // preprocess_action
+        uint32_t pa = given;
+        if (pa == A_NOTHING && st_ == S_MOVING) pa = A_FWD;
+        if (st_ == S_WAITING) pa = A_NOTHING;
+        if (pa == A_LEFT || pa == A_RIGHT) {
+          const Move mv = mv_of(pa);
+          if (!(mv.cell_ok && mv.valid)) pa = A_FWD;
+        }
+        if (is_moving_action(pa)) {
+          const Move mv = mv_of(pa);
+          if (!(mv.cell_ok && mv.valid)) pa = A_STOP;
+        }
+        if (is_moving_action(pa) && saved == 0 && st_ != S_DONE) saved = pa;
+        const bool update_allowed = (mf == 0) && pa != A_STOP;
+        desired[k] = p0;
+        uint32_t ddir = dir;
+        if (st_ == S_DONE) {
+        } else if (p0 < 0 && saved != 0) {
+          desired[k] = t_init_cell;
+          ddir = t_init_dir;
+          mover[k] = true;
+        } else if (saved != 0 && update_allowed) {
+          const Move mv = mv_of(saved);
+          desired[k] = mv.cell;
+          ddir = (uint32_t)mv.dir;
+          pa = saved;
+          mover[k] = desired[k] != p0;
+        }
+        aux[k] |= pa | (ddir << 4) | (given << 8);
+        bits[k] = tb_make(dir, st_, prev, saved, mf, tb_done(b));
       }
-      if (st_ != S_DONE && mf == 0 && m.mf_rate > 0.0) {
-        const uint64_t z = mf_draw(seed, (uint64_t)t, (uint64_t)h);
-        const double u = (double)(z >> 11) * (1.0 / 9007199254740992.0);
-        if (u < m.mf_rate)
-          mf = (uint32_t)(m.mf_min + (int32_t)(mix64(z ^ 0xA0761D6478BD642Full) % (uint64_t)(m.mf_max - m.mf_min + 1))) + 1u;
-      }
-      // preprocess_action
-      uint32_t pa = given;
-      if (pa == A_NOTHING && st_ == S_MOVING) pa = A_FWD;
-      if (st_ == S_WAITING) pa = A_NOTHING;
-      if (pa == A_LEFT || pa == A_RIGHT) {
-        const Move mv = mv_of(pa);
-        if (!(mv.cell_ok && mv.valid)) pa = A_FWD;
-      }
-      if (is_moving_action(pa)) {
-        const Move mv = mv_of(pa);
-        if (!(mv.cell_ok && mv.valid)) pa = A_STOP;
-      }
-      if (is_moving_action(pa) && saved == 0 && st_ != S_DONE) saved = pa;
-      const bool update_allowed = (mf == 0) && pa != A_STOP;
-      desired = p0;
-      uint32_t ddir = dir;
-      if (st_ == S_DONE) {
-      } else if (p0 < 0 && saved != 0) {
-        desired = t_init_cell;
-        ddir = t_init_dir;
-        mover = true;
-      } else if (saved != 0 && update_allowed) {
-        const Move mv = mv_of(saved);
-        desired = mv.cell;
-        ddir = (uint32_t)mv.dir;
-        pa = saved;
-        mover = desired != p0;
-      }
-      aux |= pa | (ddir << 4) | (given << 8);
-      bits = tb_make(dir, st_, prev, saved, mf, tb_done(b));
     }
     SFL_LAP(11);
     // pass 2: motion check, least fixed point (flatland_lite.motion_check): the lowest handle
     // wanting a cell wins it; a cell can be entered if free or its occupant moves out
-    const uint64_t M = __ballot(mover);
-    uint64_t A = 0;
-    if (M) {
+    const Mask M = mballot<TPL>(mover);
+    Mask A{};
+    if (many(M)) {
       // Bit-sliced equality instead of a loop over trains: for each bit of the cell index, one
-      // ballot of the movers' desired cells and one of the on-map trains' cells; a lane ANDs in
-      // each ballot or its complement by its own desired cell's bit, leaving exactly the movers
-      // that want the same cell (`same`) and the train that occupies it (`occs`).  One extra bit
-      // keeps an off-grid target (-1) apart from every cell.
-      uint64_t same = M, occs = __ballot(mine && pos >= 0);
-      const uint32_t dv = (uint32_t)desired;
+      // ballot (per train slot) of the movers' desired cells and one of the on-map trains'
+      // cells; a train ANDs in each ballot or its complement by its own desired cell's bit,
+      // leaving exactly the movers that want the same cell (`same`) and the train that occupies
+      // it (`occs`).  One extra bit keeps an off-grid target (-1) apart from every cell.
+      bool onmap[TPL];
+#pragma unroll
+      for (int k = 0; k < TPL; ++k) onmap[k] = mine[k] && pos[k] >= 0;
+      Mask same[TPL], occs[TPL];
+      const Mask occ0 = mballot<TPL>(onmap);
+#pragma unroll
+      for (int k = 0; k < TPL; ++k) {
+        same[k] = M;
+        occs[k] = occ0;
+      }
       for (int bi = 0; bi < m.cell_bits; ++bi) {
-        const uint64_t bd = __ballot(mover && ((dv >> bi) & 1u));
-        const uint64_t bp = __ballot(mine && pos >= 0 && (((uint32_t)pos >> bi) & 1u));
-        const bool one = (dv >> bi) & 1u;
-        same &= one ? bd : ~bd;
-        occs &= one ? bp : ~bp;
+        bool pd_[TPL], pp_[TPL];
+#pragma unroll
+        for (int k = 0; k < TPL; ++k) {
+          pd_[k] = mover[k] && (((uint32_t)desired[k] >> bi) & 1u);
+          pp_[k] = onmap[k] && (((uint32_t)pos[k] >> bi) & 1u);
+        }
+        const Mask bd = mballot<TPL>(pd_), bp = mballot<TPL>(pp_);
+#pragma unroll
+        for (int k = 0; k < TPL; ++k) {
+          const bool one = ((uint32_t)desired[k] >> bi) & 1u;
+          same[k] &= one ? bd : ~bd;
+          occs[k] &= one ? bp : ~bp;
+        }
       }
       if (m.cell_bits < 32) {  // the sign bit of an off-grid target
-        const uint64_t bd = __ballot(mover && desired < 0);
-        same &= desired < 0 ? bd : ~bd;
-        if (desired < 0) occs = 0;
+        bool pn[TPL];
+#pragma unroll
+        for (int k = 0; k < TPL; ++k) pn[k] = mover[k] && desired[k] < 0;
+        const Mask bd = mballot<TPL>(pn);
+#pragma unroll
+        for (int k = 0; k < TPL; ++k) {
+          same[k] &= desired[k] < 0 ? bd : ~bd;
+          if (desired[k] < 0) occs[k] = Mask{};
+        }
       }
       // the lowest handle wanting a cell wins it; the occupant is the (last) train on it
-      const bool win = mover && !(same & ((1ull << h) - 1ull));
-      const uint64_t occset = occs & ~(1ull << h);
-      const int occ = (mover && occset) ? 63 - __builtin_clzll(occset) : -1;
+      bool win[TPL];
+      int occ[TPL];
+#pragma unroll
+      for (int k = 0; k < TPL; ++k) {
+        const int h = lane + 64 * k;
+        win[k] = mover[k] && !many(same[k] & mbelow(Mask{}, h));
+        const Mask occset = occs[k] & ~mone(Mask{}, h);
+        occ[k] = (mover[k] && many(occset)) ? mhighest(occset) : -1;
+      }
       while (true) {
-        const bool cand = mover && win && !((A >> h) & 1ull) &&
-                          (occ < 0 || (((M >> occ) & 1ull) && ((A >> occ) & 1ull)));
-        const uint64_t nb = __ballot(cand);
-        if (!nb) break;
+        bool cand[TPL];
+#pragma unroll
+        for (int k = 0; k < TPL; ++k) {
+          const int h = lane + 64 * k;
+          cand[k] = mover[k] && win[k] && !mbit(A, h) && (occ[k] < 0 || (mbit(M, occ[k]) && mbit(A, occ[k])));
+        }
+        const Mask nb = mballot<TPL>(cand);
+        if (!many(nb)) break;
         A |= nb;
       }
     }
     SFL_LAP(12);
     // pass 3: state machine + positions, deviation fix
     const bool over = t >= m.max_episode_steps;
-    bool done = false, isdone = !mine, newly = false, dep = false;
-    if (mine) {
-      const uint32_t b = bits;
-      const int32_t p0 = pos;
-      uint32_t st_ = tb_state(b), dir = tb_dir(b), saved = tb_saved(b), mf = tb_mf(b);
-      const uint32_t pa = aux & 15u;
-      const bool in_mf = mf > 0;
-      bool ma = in_mf ? false : (mover && ((A >> h) & 1ull));
-      const bool valid_move = is_moving_action(pa) && ma;
-      const bool ed_reached = t >= t_ed;
-      const uint32_t prev_st = st_;
-      switch (st_) {
-        case S_WAITING: st_ = in_mf ? S_MF_OFF : (ed_reached ? S_READY : S_WAITING); break;
-        case S_READY: st_ = in_mf ? S_MF_OFF : (valid_move ? S_MOVING : S_READY); break;
-        case S_MF_OFF: st_ = (mf == 0) ? (ed_reached ? S_READY : S_WAITING) : S_MF_OFF; break;
-        case S_MOVING:
-          if (in_mf) st_ = S_MALF;
-          else if (pa == A_STOP) st_ = S_STOPPED;
-          else if (p0 >= 0 && p0 == t_target) st_ = S_DONE;
-          else if (!ma) st_ = S_STOPPED;
-          break;
-        case S_STOPPED: st_ = in_mf ? S_MALF : (valid_move ? S_MOVING : S_STOPPED); break;
-        case S_MALF: st_ = (mf == 0) ? (valid_move ? S_MOVING : S_STOPPED) : S_MALF; break;
-        default: break;
-      }
-      ma = ma && st_ != S_DONE;
-      int32_t np = p0;
-      if (on_map_state(st_)) {
-        if (off_map_state(prev_st)) {
-          np = t_init_cell;
-          dir = t_init_dir;
-        } else if (ma) {
-          np = desired;
-          dir = (aux >> 4) & 3u;
-          if (np == t_target) st_ = S_DONE;
+    bool done[TPL], isdone[TPL], newly[TPL], dep[TPL];
+#pragma unroll
+    for (int k = 0; k < TPL; ++k) {
+      const int h = lane + 64 * k;
+      const int32_t t_ed = tt0[k][0], t_target = tt0[k][3], t_init_cell = tt1[k][0];
+      const uint32_t t_init_dir = (uint32_t)tt1[k][3] & 0xFFu;
+      done[k] = false;
+      isdone[k] = !mine[k];
+      newly[k] = false;
+      dep[k] = false;
+      if (mine[k]) {
+        const uint32_t b = bits[k];
+        const int32_t p0 = pos[k];
+        uint32_t st_ = tb_state(b), dir = tb_dir(b), saved = tb_saved(b), mf = tb_mf(b);
+        const uint32_t pa = aux[k] & 15u;
+        const bool in_mf = mf > 0;
+        bool ma = in_mf ? false : (mover[k] && mbit(A, h));
+        const bool valid_move = is_moving_action(pa) && ma;
+        const bool ed_reached = t >= t_ed;
+        const uint32_t prev_st = st_;
+        switch (st_) {
+          case S_WAITING: st_ = in_mf ? S_MF_OFF : (ed_reached ? S_READY : S_WAITING); break;
+          case S_READY: st_ = in_mf ? S_MF_OFF : (valid_move ? S_MOVING : S_READY); break;
+          case S_MF_OFF: st_ = (mf == 0) ? (ed_reached ? S_READY : S_WAITING) : S_MF_OFF; break;
+          case S_MOVING:
+            if (in_mf) st_ = S_MALF;
+            else if (pa == A_STOP) st_ = S_STOPPED;
+            else if (p0 >= 0 && p0 == t_target) st_ = S_DONE;
+            else if (!ma) st_ = S_STOPPED;
+            break;
+          case S_STOPPED: st_ = in_mf ? S_MALF : (valid_move ? S_MOVING : S_STOPPED); break;
+          case S_MALF: st_ = (mf == 0) ? (valid_move ? S_MOVING : S_STOPPED) : S_MALF; break;
+          default: break;
         }
-      }
-      if (st_ == S_DONE && !((arr_mask >> h) & 1ull)) {
-        newly = true;  // arrived: position None, arrival_time set
-        np = -1;
-      }
-      if (mf > 0) mf -= 1;
-      if (np >= 0) saved = 0;
-      done = (st_ == S_DONE) || over;
-      isdone = st_ == S_DONE;
-      pos = np;
-      // switchfl: deviation fix
-      if ((aux >> 12) & 1u) {
-        const uint32_t given = (aux >> 8) & 15u;
-        if (pred != np && ((aux >> 13) & 1u) && given != A_STOP) {
-          plan = pl_push_front(plan, given, lerr);
-          if ((aux >> 14) & 1u) nprv = (nprv & 0xFFFF0000u) | (sdec & 0xFFFFu);
+        ma = ma && st_ != S_DONE;
+        int32_t np = p0;
+        if (on_map_state(st_)) {
+          if (off_map_state(prev_st)) {
+            np = t_init_cell;
+            dir = t_init_dir;
+          } else if (ma) {
+            np = desired[k];
+            dir = (aux[k] >> 4) & 3u;
+            if (np == t_target) st_ = S_DONE;
+          }
         }
+        if (st_ == S_DONE && !mbit(arr_mask, h)) {
+          newly[k] = true;  // arrived: position None, arrival_time set
+          np = -1;
+        }
+        if (mf > 0) mf -= 1;
+        if (np >= 0) saved = 0;
+        done[k] = (st_ == S_DONE) || over;
+        isdone[k] = st_ == S_DONE;
+        pos[k] = np;
+        // switchfl: deviation fix
+        if ((aux[k] >> 12) & 1u) {
+          const uint32_t given = (aux[k] >> 8) & 15u;
+          if (pred[k] != np && ((aux[k] >> 13) & 1u) && given != A_STOP) {
+            plan[k] = pl_push_front(plan[k], given, lerr);
+            if ((aux[k] >> 14) & 1u) nprv[k] = (nprv[k] & 0xFFFF0000u) | (sdec[k] & 0xFFFFu);
+          }
+        }
+        dep[k] = t == t_ed - 2;
+        bits[k] = tb_make(dir, st_, tb_prev(b), saved, mf, done[k] ? 1u : 0u);
       }
-      dep = t == t_ed - 2;
-      bits = tb_make(dir, st_, tb_prev(b), saved, mf, done ? 1u : 0u);
     }
-    arr_mask |= __ballot(newly);
+    arr_mask |= mballot<TPL>(newly);
     SFL_LAP(13);
     // delete the semaphores of done trains (switch_env.py:370-376): each lane its own records
-    const uint64_t DONE = __ballot(done);
-    if (DONE) {
+    const Mask DONE = mballot<TPL>(done);
+    if (many(DONE)) {
 #pragma unroll
       for (int k = 0; k < PPL; ++k) {
         const uint32_t r = sem(k);
-        sem(k) = (r_present(r) & (((DONE >> r_owner(r)) & 1ull) != 0ull)) ? 0u : r;
+        sem(k) = (r_present(r) & mbit(DONE, (int)r_owner(r))) ? 0u : r;
       }
     }
     // departure semaphores, in handle order (switch_env.py:379-384)
-    uint64_t D = __ballot(dep);
-    while (D) {
-      const int j = ctz64(D);
-      D &= D - 1ull;
+    Mask D = mballot<TPL>(dep);
+    while (many(D)) {
+      const int j = mctz(D);
+      mclear_low(D);
       const int32_t ed = ltt[8 * j];
-      sset((int)(rl(nprv, j) & 0xFFFFu), r_pack(j, 1, ed - 2, ed + ldc(m.tr_pack, (size_t)j * 8 + 5)));
+      sset((int)(trl(nprv, j) & 0xFFFFu), r_pack(j, 1, ed - 2, ed + ldc(m.tr_pack, (size_t)j * 8 + 5)));
     }
     // pass 4: extend_semaphores (rail_network.py:229-244)
-    const uint32_t st4 = tb_state(bits);
-    const uint64_t SM = __ballot(mine && (st4 == S_STOPPED || st4 == S_MALF));
-    if (SM) {
+    bool smp[TPL], map_[TPL], mfp[TPL];
+#pragma unroll
+    for (int k = 0; k < TPL; ++k) {
+      const uint32_t st4 = tb_state(bits[k]);
+      smp[k] = mine[k] && (st4 == S_STOPPED || st4 == S_MALF);
+      map_[k] = mine[k] && st4 == S_MALF;
+      mfp[k] = mine[k] && tb_mf(bits[k]) > 0;
+    }
+    const Mask SM = mballot<TPL>(smp);
+    if (many(SM)) {
 #pragma unroll
       for (int k = 0; k < PPL; ++k) {
         const uint32_t r = sem(k);
-        const bool ext = r_present(r) & (((SM >> r_owner(r)) & 1ull) != 0ull);
+        const bool ext = r_present(r) & mbit(SM, (int)r_owner(r));
         sem(k) = ext ? r_pack(r_owner(r), r_in(r), t, t + (r_t1(r) - r_t0(r))) : r;
       }
     }
-    uint64_t MA = __ballot(mine && st4 == S_MALF);
-    while (MA) {
-      const int j = ctz64(MA);
-      MA &= MA - 1ull;
-      const int p = (int)(rl(nprv, j) & 0xFFFFu);
+    Mask MA = mballot<TPL>(map_);
+    while (many(MA)) {
+      const int j = mctz(MA);
+      mclear_low(MA);
+      const int p = (int)(trl(nprv, j) & 0xFFFFu);
       if (!r_present(sget(p))) sset(p, r_pack(j, 1, t, t + ldc(m.tr_pack, (size_t)j * 8 + 5)));
     }
     // malfunction count (switch_env.py:399-401)
-    const uint64_t MF = __ballot(mine && tb_mf(bits) > 0);
-    n_mf += popc64(MF & ~mf_mask);
+    const Mask MF = mballot<TPL>(mfp);
+    n_mf += mpopc(MF & ~mf_mask);
     mf_mask = MF;
     SFL_LAP(14);
     // _check_active_switch (switch_env.py:427-485)
-    bool act = false;
-    if (mine && pos >= 0 && st4 != S_WAITING) {
-      const uint32_t nxt = pl_len(plan) ? pl_front(plan) : A_FWD;
-      const Move mv = check_action<false>(nxt, pos, (int)tb_dir(bits));
-      if (mv.cell >= 0) {
-        const int sw_at = dest_sw(mv);
-        if (sw_at >= 0) {
-          int sw = -1;
-          if (st4 == S_READY || st4 == S_MOVING) sw = sw_at;
-          else if ((st4 == S_STOPPED || st4 == S_MALF) && tb_prev(bits) == A_STOP) sw = sw_at;
-          else if (st4 == S_STOPPED || st4 == S_MALF) sw = (int)((nprv & 0xFFFFu) >> 2);
-          if (sw >= m.S) {  // next port is None: the reference would raise here
-            lerr |= E_PORT;
-          } else if (sw >= 0) {
-            act = true;
-            sdec = (sdec & 0xFFFFu) | ((uint32_t)sw << 16);
+    bool act[TPL];
+#pragma unroll
+    for (int k = 0; k < TPL; ++k) {
+      act[k] = false;
+      const uint32_t st4 = tb_state(bits[k]);
+      if (mine[k] && pos[k] >= 0 && st4 != S_WAITING) {
+        const uint32_t nxt = pl_len(plan[k]) ? pl_front(plan[k]) : A_FWD;
+        const Move mv = check_action<false>(nxt, pos[k], (int)tb_dir(bits[k]));
+        if (mv.cell >= 0) {
+          const int sw_at = dest_sw(mv);
+          if (sw_at >= 0) {
+            int sw = -1;
+            if (st4 == S_READY || st4 == S_MOVING) sw = sw_at;
+            else if ((st4 == S_STOPPED || st4 == S_MALF) && tb_prev(bits[k]) == A_STOP) sw = sw_at;
+            else if (st4 == S_STOPPED || st4 == S_MALF) sw = (int)((nprv[k] & 0xFFFFu) >> 2);
+            if (sw >= m.S) {  // next port is None: the reference would raise here
+              lerr |= E_PORT;
+            } else if (sw >= 0) {
+              act[k] = true;
+              sdec[k] = (sdec[k] & 0xFFFFu) | ((uint32_t)sw << 16);
+            }
           }
         }
       }
     }
-    q_mask = __ballot(act);
+    q_mask = mballot<TPL>(act);
     SFL_LAP(15);
-    const uint64_t full = (m.T == 64) ? ~0ull : ((1ull << m.T) - 1ull);
-    const uint64_t ALL = __ballot(isdone);
+    const Mask full = mfirst(Mask{}, m.T);
+    const Mask ALL = mballot<TPL>(isdone);
     ep_ticks += 1;
     if ((ALL & full) == full || over) flags |= F_TERM;
   }
@@ -841,27 +962,34 @@ struct WEnv {
   // Q values are dropped when the batch writes their cell (pf_written).  Slot words are never
   // stale: a decision writes only its own train's slots and a train decides once per batch.
   __device__ __forceinline__ void prefetch(bool greedy) {
-    const uint64_t malf = __ballot(mine && tb_state(bits) == S_MALF);
-    pf_roff = pf_qoff = PF_NONE;
-    if (!((q_mask >> lane) & 1ull)) return;
+    const Mask malf = malf_mask();
+#pragma unroll
+    for (int k = 0; k < TPL; ++k) {
+      pf_roff[k] = pf_qoff[k] = PF_NONE;
+      if (mbit(q_mask, lane + 64 * k)) prefetch_slot(k, malf, greedy);
+    }
+  }
+  // train slot ks of this lane (train lane + 64 ks) is queued: stage its decision's inputs
+  __device__ __forceinline__ void prefetch_slot(int ks, Mask malf, bool greedy) {
+    const int hk = lane + 64 * ks;
     // Loads are issued by dependency level, unconditionally (clamped indices), so the chains
-    // overlap: level 1 needs only this lane's registers, level 2 the level-1 results, ...
-    const int sw = (int)(sdec >> 16);
-    const int pin = (int)(nprv & 0xFFFFu);
+    // overlap: level 1 needs only this train's registers, level 2 the level-1 results, ...
+    const int sw = (int)(sdec[ks] >> 16);
+    const int pin = (int)(nprv[ks] & 0xFFFFu);
     const int slot = pin & 3;
-    const int dir0 = (int)tb_dir(bits);
-    const int pos0 = pos >= 0 ? pos : 0;
-    double* pfl = lpf + PF_W * lane;
+    const int dir0 = (int)tb_dir(bits[ks]);
+    const int pos0 = pos[ks] >= 0 ? pos[ks] : 0;
+    double* pfl = lpf + PF_W * hk;
     int32_t* pfi = (int32_t*)pfl + PF_I;
     // level 1: slot word, switch record, timetable row, the row block's port record, first moves
-    const uint64_t slw = ld(slotb, slot_ix(sw, lane));
+    const uint64_t slw = ld(slotb, slot_ix(sw, hk));
     const u4 w0 = ld((const u4*)m.sw_pack, (size_t)sw * 4u);
     const u4 w4 = ld((const u4*)m.sw_pack, (size_t)sw * 4u + 1u);  // compact-row descriptors
     const vec_t<uint32_t, 2> nbw = ld((const vec_t<uint32_t, 2>*)m.sw_pack, (size_t)sw * 8u + 4u);
-    const vec_t<int32_t, 4> trw = *(const vec_t<int32_t, 4>*)(ltt + 8 * lane);  // ed, la, k, target
+    const vec_t<int32_t, 4> trw = *(const vec_t<int32_t, 4>*)(ltt + 8 * hk);  // ed, la, k, target
     const u4 pr = ld((const u4*)m.port_pack, (size_t)(4 * sw + slot));
-    const uint32_t n_plan = pl_len(plan);
-    const uint32_t a1 = n_plan ? pl_front(plan) : A_FWD;
+    const uint32_t n_plan = pl_len(plan[ks]);
+    const uint32_t a1 = n_plan ? pl_front(plan[ks]) : A_FWD;
     // move-table rows (all four rail actions) at the cell and after the first rail action
     const u4 row0 = ld((const u4*)m.move_tab, (size_t)((uint32_t)pos0 * 4u + (uint32_t)dir0));
     auto mv_in = [](const u4& r, uint32_t a) -> Move {
@@ -871,11 +999,11 @@ struct WEnv {
     // distances the decision needs (reward_func.py:23-78): at the cell, along the STOP plan
     // ([STOP] + plan) and along each route's plan ([front or FWD, final rail action 1..3])
     const int32_t la = (int32_t)trw[1], k = (int32_t)trw[2];
-    const int32_t dd = dist_v(k, pos, dir0);
+    const int32_t dd = dist_v(k, pos[ks], dir0);
     {
-      int pc = pos, pd = dir0;
+      int pc = pos[ks], pd = dir0;
       for (uint32_t i = 0; i < n_plan; ++i) {
-        const uint32_t a = pl_at(plan, i);
+        const uint32_t a = pl_at(plan[ks], i);
         if (i == 0 && a != A_STOP && pc >= 0) {
           const Move mv = mv_in(row0, a);
           pc = mv.cell;
@@ -887,8 +1015,8 @@ struct WEnv {
       pfi[1] = dist_v(k, pc, pd);
     }
     {
-      int pc = pos, pd = dir0;
-      if (a1 != A_STOP && pos >= 0) {
+      int pc = pos[ks], pd = dir0;
+      if (a1 != A_STOP && pos[ks] >= 0) {
         const Move m1 = mv_in(row0, a1);
         pc = m1.cell;
         pd = m1.dir;
@@ -917,7 +1045,7 @@ struct WEnv {
     for (int j = 0; j < 4; ++j) {
       const int p = 4 * sw + j;
       const int nb = j < np ? (int)((nbw[j >> 1] >> (16 * (j & 1))) & 0xFFFFu) : p;
-      const uint32_t blk = rec_blocks(lsem[nb], (uint32_t)lane, malf, 0u) | rec_blocks(lsem[p], (uint32_t)lane, malf, 1u);
+      const uint32_t blk = rec_blocks(lsem[nb], (uint32_t)hk, malf, 0u) | rec_blocks(lsem[p], (uint32_t)hk, malf, 1u);
       fb |= (blk == 0u && j < np) ? (1u << j) : 0u;
     }
     const int32_t dl = now - la + dd;
@@ -925,7 +1053,7 @@ struct WEnv {
     const uint32_t lvl = dl <= 0 ? 0u : (dl <= avail * 20 ? 1u : 2u);
     const uint32_t state = ((fb * (uint32_t)m.K) + (uint32_t)k) * 3u + lvl;
     const uint32_t w = pr[1] >> 16, roff = pr[3] + state * w;
-    const bool row_ok = pos >= 0 && dd < DIST_INF && (pin >> 2) == sw && slot < np;
+    const bool row_ok = pos[ks] >= 0 && dd < DIST_INF && (pin >> 2) == sw && slot < np;
     const uint32_t qoff = pp[3] + ((pend >> 14) & 0x3FFFu) * (pp[1] >> 16) + ((pend >> 28) & 3u);
     // level 3: Q values
     const double* rp = qbase() + (row_ok ? roff : 0u);
@@ -970,13 +1098,16 @@ struct WEnv {
     }
     pfl[4] = qv;
     pfl[5] = __longlong_as_double((long long)slw);
-    pf_roff = row_ok ? roff : PF_NONE;
-    pf_qoff = hp ? qoff : PF_NONE;
+    pf_roff[ks] = row_ok ? roff : PF_NONE;
+    pf_qoff[ks] = hp ? qoff : PF_NONE;
   }
   // a Q cell of this env was written (uniform offset): drop staged copies that contain it
   __device__ __forceinline__ void pf_written(uint32_t off) {
-    pf_qoff = (pf_qoff == off) ? PF_NONE : pf_qoff;
-    pf_roff = (off - pf_roff < 4u) ? PF_NONE : pf_roff;
+#pragma unroll
+    for (int k = 0; k < TPL; ++k) {
+      pf_qoff[k] = (pf_qoff[k] == off) ? PF_NONE : pf_qoff[k];
+      pf_roff[k] = (off - pf_roff[k] < 4u) ? PF_NONE : pf_roff[k];
+    }
   }
 
   // ---- decision (wave-uniform): observe (observer.py:246-308), epsilon-greedy
@@ -1008,9 +1139,9 @@ struct WEnv {
     }
     SFL_LAP(0);
     SFL_PCNT(8);
-    const int h = ctz64(q_mask);
-    q_mask &= q_mask - 1ull;
-    const uint32_t sd = rl(sdec, h);
+    const int h = mctz(q_mask);
+    mclear_low(q_mask);
+    const uint32_t sd = trl(sdec, h);
     const int sw = (int)(sd >> 16);
     const SwRec swr = sw_rec(sw);
     const vec_t<int32_t, 8> tr = ldcv<vec_t<int32_t, 8>>(m.tr_pack, (size_t)h);
@@ -1029,10 +1160,10 @@ struct WEnv {
 #pragma unroll
     for (int i = 0; i < 5; ++i) rng_w[i] = lrng[i];
     const uint32_t n_sw = cget(sw);
-    const uint32_t pf_roff_h = rl(pf_roff, h), pf_qoff_h = rl(pf_qoff, h);
+    const uint32_t pf_roff_h = trl(pf_roff, h), pf_qoff_h = trl(pf_qoff, h);
     const int np = swr.np();
     const int na = swr.na();
-    const uint32_t npv = rl(nprv, h);
+    const uint32_t npv = trl(nprv, h);
     const int pin = (int)(npv & 0xFFFFu);
     const int pprev = (int)(npv >> 16);
     int slot = pin & 3;
@@ -1049,13 +1180,13 @@ struct WEnv {
     const uint32_t nbl = ((lane & 2) ? nbw[1] : nbw[0]) >> ((lane & 1) * 16);
     const bool pvalid = lane < np;
     const int nbj = pvalid ? (int)(nbl & 0xFFFFu) : pj;
-    const uint64_t malf = __ballot(mine && tb_state(bits) == S_MALF);
+    const Mask malf = malf_mask();
     const uint32_t rn = lsem[nbj], ro = lsem[pj];
     const uint32_t blk = rec_blocks(rn, (uint32_t)h, malf, 0u) | rec_blocks(ro, (uint32_t)h, malf, 1u);
     const uint32_t free_bits = (uint32_t)__ballot(pvalid && blk == 0u) & 15u;
     SFL_LAP(2);
-    const uint32_t b = rl(bits, h);
-    const int32_t p0 = rl(pos, h);
+    const uint32_t b = trl(bits, h);
+    const int32_t p0 = trl(pos, h);
     const int32_t ed = tr[0], la = tr[1], k = tr[2];
     const int32_t dl = now - la + dist_staged(uni(pfd01[0]));
     const int32_t avail = la - ed;
@@ -1254,7 +1385,7 @@ struct WEnv {
       tset(nprv, h, (uint32_t)target | ((uint32_t)out_p << 16));
       next_sw = target >> 2;
     }
-    uint32_t p = rl(plan, h);
+    uint32_t p = trl(plan, h);
     if (moving && pl_len(p) > 0) {
       p = (p & 0xF0u) | 1u;  // plan[:1]
       p = pl_push_back(p, turn, lerr);
@@ -1278,7 +1409,7 @@ struct WEnv {
     const uint32_t tq = turn & 3u;
     const int32_t dproj = moving ? (tq == 0 ? pfd23[0] : tq == 1 ? pfd23[1] : tq == 2 ? pfd45[0] : pfd45[1]) : pfd01[1];
     const int32_t cur = now - la + dist_staged(uni(dproj));
-    const int32_t diff = rl(delay, h) - cur;
+    const int32_t diff = trl(delay, h) - cur;
     d.r_new = (pl_front(p) == A_STOP && !all_blocked) ? diff - 1300 : diff;
     tset(delay, h, cur);
     d.sw = sw;
@@ -1340,12 +1471,12 @@ struct WEnv {
     // destination bonus for newly arrived trains (distr_q.py:344-356); lanes take switches.
     // Distinct slots of one train never hold the same Q cell (same cell => same action =>
     // same successor switch => same slot), so the lanes' updates are independent.
-    uint64_t fresh = arr_mask & ~fl_mask;
+    Mask fresh = arr_mask & ~fl_mask;
     fl_mask |= fresh;
-    if (fresh) pf_ok = false;  // bonus writes: stage the rest of the batch again
-    while (fresh) {
-      const int tr = ctz64(fresh);
-      fresh &= fresh - 1ull;
+    if (many(fresh)) pf_ok = false;  // bonus writes: stage the rest of the batch again
+    while (many(fresh)) {
+      const int tr = mctz(fresh);
+      mclear_low(fresh);
       for (int base = 0; base < m.S; base += 64) {
         const int sw2 = base + lane;
         const bool valid = sw2 < m.S;
@@ -1394,7 +1525,8 @@ __device__ void run(const SflMap& m, const SflState& s, const SflCtl& c) {
   const int lane = (int)__lane_id();
   const uint32_t e = uni((uint32_t)((blockIdx.x * blockDim.x + threadIdx.x) >> 6));
   if (e >= s.E) return;
-  __shared__ uint32_t lds[(SFL_WAVE_BLOCK / 64) * LDS_WORDS];
+  constexpr int WPB = TW > 64 ? 1 : SFL_WAVE_BLOCK / 64;  // waves (envs) per block (sfl.hip launches)
+  __shared__ uint32_t lds[WPB * LDS_WORDS];
   V v(m, s, e, lane, lds + (threadIdx.x >> 6) * LDS_WORDS);
   v.load();
   int32_t phase = uni(ld(s.phase, e));
@@ -1432,13 +1564,13 @@ __device__ void run(const SflMap& m, const SflState& s, const SflCtl& c) {
       SFL_PACC(0, t0);
       phase = PH_TICK;
     } else if (phase == PH_TICK) {
-      abytes += 36u * (uint32_t)(m.T - popc64(v.arr_mask));
+      abytes += 36u * (uint32_t)(m.T - mpopc(v.arr_mask));
       SFL_PT(t0);
       v.tick();
       SFL_PACC(1, t0);
       ticks++;
       if (v.flags & F_TERM) phase = (v.flags & F_INFLIGHT) ? PH_POST : PH_END;
-      else if (v.q_mask) phase = (v.flags & F_INFLIGHT) ? PH_POST : PH_DECIDE;
+      else if (many(v.q_mask)) phase = (v.flags & F_INFLIGHT) ? PH_POST : PH_DECIDE;
     } else if (phase == PH_DECIDE || phase == PH_POST) {
       const bool greedy = (v.flags & F_GREEDY) != 0;
       // post step + loop bookkeeping of decision d; true: the launch's decision budget is spent
@@ -1481,7 +1613,7 @@ __device__ void run(const SflMap& m, const SflState& s, const SflCtl& c) {
           SFL_PACC(2, t0);
           abytes += d.abytes;
           v.flags |= F_INFLIGHT;
-          if (!v.q_mask) {
+          if (!many(v.q_mask)) {
             phase = PH_TICK;
             break;
           }
@@ -1492,7 +1624,7 @@ __device__ void run(const SflMap& m, const SflState& s, const SflCtl& c) {
       }
       if (stop) break;
     } else {  // PH_END
-      const int arrived = popc64(v.arr_mask);
+      const int arrived = mpopc(v.arr_mask);
       const size_t cap = (size_t)(c.stats_cap > 0 ? c.stats_cap : 1);
       const bool greedy = (v.flags & F_GREEDY) != 0;
       if (c.st_cum && c.stats_cap > 0 && (!greedy || test_mode)) {
@@ -1505,7 +1637,9 @@ __device__ void run(const SflMap& m, const SflState& s, const SflCtl& c) {
           st(c.st_dec, row * s.E + e, v.ep_dec);
           st(c.st_ticks, row * s.E + e, v.ep_ticks);
         }
-        if (v.mine) st(c.st_delays, (row * m.T + lane) * s.E + e, v.delay);
+#pragma unroll
+        for (int k = 0; k < V::TPL; ++k)
+          if (v.mine[k]) st(c.st_delays, (row * m.T + lane + 64 * k) * s.E + e, v.delay[k]);
       }
       if (greedy && !test_mode && c.sx_cum && c.stats_cap > 0 && lane == 0) {
         const size_t row = (size_t)(ep_t - c.stats_base) % cap;

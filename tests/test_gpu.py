@@ -126,13 +126,14 @@ def test_c3_full_size_batch(lib):
     b.close()
 
 
-def test_c5_small_batch(lib):
-    """256-switch / 128-train map (max trains per env), a few envs against the oracle."""
+def test_c5_small_batch(lib, kernel):
+    """256-switch / 128-train map (max trains per env, two train slots per lane in k_wave), a few
+    envs against the oracle, on both kernels."""
     sc = mapgen.make_config("c5")
     cm = comp.compile_scenario(sc)
     seeds = [5, 6, 7, 8]
     b = runtime.Batch(cm, HP, seeds, lib=lib, ntab=1 << 14)
-    assert b.counters()["kernel_variant"] == 0  # 128 trains: lane-per-env kernel
+    _check_kernel(b, kernel)
     b.learn_begin()
     b.apply_qinit()
     b.step(150)
@@ -169,7 +170,8 @@ def test_partitioned_rounds_gpu_equal_fused(lib, cfg, E):
     ref.close()
 
 
-@pytest.mark.parametrize("S,T,variant", [(64, 48, 3), (100, 48, 4), (120, 64, 4)])
+@pytest.mark.parametrize("S,T,variant", [(64, 48, 3), (100, 48, 4), (120, 64, 4), (100, 100, 5), (200, 40, 5),
+                                         (256, 128, 5)])
 def test_wave_kernel_shapes(lib, S, T, variant):
     """Every k_wave shape (sfl::kVariants: more trains per env, more ports / switches per lane)
     bit-equal to the host build of the lane kernel, and sampled envs to the oracle."""
