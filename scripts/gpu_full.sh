@@ -4,7 +4,7 @@ cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 OUT=gpurun_out/${TAG:-full}
 mkdir -p $OUT
-timeout -k 10 900 python -m pytest tests/test_gpu.py -x -q > $OUT/pytest_gpu.log 2>&1; rc=$?; echo "pytest rc=$rc"; tail -3 $OUT/pytest_gpu.log
+timeout -k 10 900 python -u -m pytest tests/test_gpu.py -x -v --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1; rc=$?; echo "pytest rc=$rc"; tail -3 $OUT/pytest_gpu.log
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python __graft_entry__.py > $OUT/smoke.log 2>&1; echo "smoke rc=$?"; tail -1 $OUT/smoke.log
 timeout -k 10 300 python test_model.py $OUT/test_model --episodes 5 > $OUT/test_model.log 2>&1; echo "test_model rc=$?"; tail -4 $OUT/test_model.log
