@@ -48,6 +48,20 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
   sfl::wave::run<PPL, SPL, TW, TRACE>(*m, *s, *c);
 }
 
+// graph-partitioned rounds, local env step on the one-env-per-wave body (sfl_wave.h, PART)
+template <int PPL, int SPL, int TW>
+__global__ void __launch_bounds__(SFL_WAVE_BLOCK) __attribute__((amdgpu_waves_per_eu(SFL_WAVE_OCC)))
+k_wave_part(const sfl::SflMap* __restrict__ m, const sfl::SflState* __restrict__ s, const sfl::SflCtl* __restrict__ c,
+            const sfl::SflPart* __restrict__ P) {
+  sfl::wave::run<PPL, SPL, TW, false, true>(*m, *s, *c, P);
+}
+template <int PPL, int SPL, int TW>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
+k_wave2_part(const sfl::SflMap* __restrict__ m, const sfl::SflState* __restrict__ s, const sfl::SflCtl* __restrict__ c,
+             const sfl::SflPart* __restrict__ P) {
+  sfl::wave::run<PPL, SPL, TW, false, true>(*m, *s, *c, P);
+}
+
 // graph-partitioned rounds (sfl_part.h): local env step (lane per env), segment headers,
 // owner-side answer and update (one thread per record)
 template <int NW>
@@ -328,13 +342,24 @@ struct HipBackend {
     check(hipStreamSynchronize(stream), "params sync");
     return (PartParams*)d_pparams;
   }
-  int part_local(const sfl::SflMap& m, const sfl::SflState& s, const sfl::SflCtl& c, const sfl::SflPart& P, float* ms) {
+  int part_local(const sfl::SflMap& m, const sfl::SflState& s, const sfl::SflCtl& c, const sfl::SflPart& P, int variant,
+                 float* ms) {
     PartParams* pp = part_params(m, s, c, P);
     if (!pp) return -1;
     check(hipEventRecord(ev0, stream), "event");
     // one wave per block: a round's envs spread over as many CUs as possible
     const unsigned blocks = (s.E + 63) / 64;
-    if (m.T <= 32) k_part_local<1><<<blocks, 64, 0, stream>>>(&pp->m, &pp->s, &pp->c, &pp->P);
+    const unsigned wblocks = (unsigned)(((size_t)s.E * 64 + SFL_WAVE_BLOCK - 1) / SFL_WAVE_BLOCK);
+#define SFL_KWP(v) \
+  k_wave_part<sfl::kVariants[v].PPL, sfl::kVariants[v].SPL, sfl::kVariants[v].TW><<<wblocks, SFL_WAVE_BLOCK, 0, stream>>>(&pp->m, &pp->s, &pp->c, &pp->P)
+    if (variant == 1) SFL_KWP(1);
+    else if (variant == 2) SFL_KWP(2);
+    else if (variant == 3) SFL_KWP(3);
+    else if (variant == 4) SFL_KWP(4);
+    else if (variant == 5)
+      k_wave2_part<sfl::kVariants[5].PPL, sfl::kVariants[5].SPL, sfl::kVariants[5].TW><<<s.E, 64, 0, stream>>>(&pp->m, &pp->s, &pp->c, &pp->P);
+#undef SFL_KWP
+    else if (m.T <= 32) k_part_local<1><<<blocks, 64, 0, stream>>>(&pp->m, &pp->s, &pp->c, &pp->P);
     else if (m.T <= 64) k_part_local<2><<<blocks, 64, 0, stream>>>(&pp->m, &pp->s, &pp->c, &pp->P);
     else k_part_local<4><<<blocks, 64, 0, stream>>>(&pp->m, &pp->s, &pp->c, &pp->P);
     if (!check(hipGetLastError(), "k_part_local")) return -1;

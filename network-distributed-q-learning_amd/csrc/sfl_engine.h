@@ -610,8 +610,8 @@ int part_config(Handle<B>* h, int rank, int world, const int32_t* owner, uint32_
   h->be.fill_f64(P.q_own, h->map.default_q, (size_t)E_tot * off);
   h->be.memset(P.touched_own, 0, (size_t)E_tot * P.own_words * 4);
   h->be.memset(P.dec_done, 0, h->E * 8);
-  // the partitioned rounds run the lane-per-env body: its (switch, train) slot layout
-  h->variant = 0;
+  // the partitioned rounds run the body the handle was created for (h->variant: k_wave where
+  // eligible, else the lane-per-env body), with that body's (switch, train) slot layout
   return h->be.sync() ? fail(h->be.error()) : 0;
 }
 
@@ -718,7 +718,7 @@ int part_local(Handle<B>* h, int64_t budget, const void* rep_in, void* req_out, 
   c.launch_ticks = h->d_launch_ticks;
   c.launch_bytes = h->d_launch_bytes;
   float ms = 0.f;
-  int rc = h->be.part_local(h->map, h->st, c, P, &ms);
+  int rc = h->be.part_local(h->map, h->st, c, P, h->variant, &ms);
   h->last_kernel_ms = ms;
   std::vector<uint32_t> cnt(2 * (size_t)P.world + 1);
   h->be.d2h(cnt.data(), P.cnt, cnt.size() * 4);

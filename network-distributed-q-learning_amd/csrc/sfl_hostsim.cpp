@@ -69,7 +69,8 @@ struct HostBackend {
   void replicate(void* base, size_t bytes, uint32_t n) {
     for (uint32_t i = 1; i < n; ++i) memcpy((char*)base + (size_t)i * bytes, base, bytes);
   }
-  int part_local(const sfl::SflMap& m, const sfl::SflState& s, const sfl::SflCtl& c, const sfl::SflPart& P, float* ms) {
+  int part_local(const sfl::SflMap& m, const sfl::SflState& s, const sfl::SflCtl& c, const sfl::SflPart& P, int /*variant*/,
+                 float* ms) {
 #pragma omp parallel for schedule(dynamic, 1)
     for (int64_t e = 0; e < (int64_t)s.E; ++e) {
       if (m.T <= 32) sfl::env_run_part<1>(m, s, c, P, (uint32_t)e);

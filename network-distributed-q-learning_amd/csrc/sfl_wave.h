@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 
 #include "sfl_core.h"
+#include "sfl_part.h"
 
 namespace sfl {
 namespace wave {
@@ -212,12 +213,17 @@ struct PortRec {
   __device__ __forceinline__ uint32_t q_off() const { return w[3]; }
 };
 // PPL semaphore registers (ports <= 64*PPL) and SPL counter registers (switches <= 64*SPL) per lane
-template <int PPL, int SPL, int TWc>
+// PART: the graph-partitioned mode's local step (sfl_part.h): the env's Q rows live on their
+// switches' owner ranks, so a decision is observed in one launch (request to the owner) and
+// applied in the next (with the owner's reply), and the post step's Q operations are update
+// records to the owners
+template <int PPL, int SPL, int TWc, bool PART = false>
 struct WEnv {
   const SflMap& m;
   const SflState& s;
   const uint32_t e, E;
   const int lane;
+  const SflPart* P;  // PART only
   static constexpr int TPL = (TWc + 63) / 64;  // train slots per lane: trains lane, lane + 64
   using Mask = typename MaskOf<TPL>::type;
   bool mine[TPL];  // lane + 64 k < T: slot k holds train lane + 64 k
@@ -264,8 +270,8 @@ struct WEnv {
   uint64_t lap_t = 0;
 #endif
 
-  __device__ WEnv(const SflMap& m_, const SflState& s_, uint32_t e_, int lane_, uint32_t* lds)
-      : m(m_), s(s_), e(e_), E(s_.E), lane(lane_), lsem(lds), lcnt(lds + 64 * PPL), lpf((double*)(lds + 64 * (PPL + SPL))) {
+  __device__ WEnv(const SflMap& m_, const SflState& s_, uint32_t e_, int lane_, uint32_t* lds, const SflPart* P_ = nullptr)
+      : m(m_), s(s_), e(e_), E(s_.E), lane(lane_), P(P_), lsem(lds), lcnt(lds + 64 * PPL), lpf((double*)(lds + 64 * (PPL + SPL))) {
 #pragma unroll
     for (int k = 0; k < TPL; ++k) {
       mine[k] = lane_ + 64 * k < m_.T;
@@ -281,6 +287,12 @@ struct WEnv {
   __device__ __forceinline__ uint32_t slot_ix(int sw, int h) const { return (uint32_t)(h * m.S + sw); }
 
   __device__ __forceinline__ size_t ix(size_t i) const { return i * (size_t)E + e; }
+  // per-train / per-port / per-switch state between launches: env-major ([E][T], [E][NP], [E][S];
+  // sfl_get_env_state), so a wave's load and store of its env are contiguous (the lane-per-env
+  // body keeps the env index fastest instead)
+  __device__ __forceinline__ size_t tix(int h) const { return (size_t)e * (uint32_t)m.T + (uint32_t)h; }
+  __device__ __forceinline__ size_t pix(int p) const { return (size_t)e * (uint32_t)m.NP + (uint32_t)p; }
+  __device__ __forceinline__ size_t cix(int sw) const { return (size_t)e * (uint32_t)m.S + (uint32_t)sw; }
 
   // ---- cross-lane access (index wave-uniform) -------------------------------------
   __device__ __forceinline__ uint32_t sget(int p) const { return uni(lsem[p]); }
@@ -483,12 +495,12 @@ struct WEnv {
     for (int k = 0; k < TPL; ++k) {
       const int hk = lane + 64 * k;
       if (mine[k]) {
-        pos[k] = ld(s.tr_pos, ix(hk));
-        bits[k] = ld(s.tr_bits, ix(hk));
-        plan[k] = ld(s.tr_plan, ix(hk));
-        nprv[k] = (uint32_t)ld(s.tr_next, ix(hk)) | ((uint32_t)ld(s.tr_prev, ix(hk)) << 16);
-        sdec[k] = (uint32_t)ld(s.tr_src, ix(hk)) | ((uint32_t)ld(s.tr_dec, ix(hk)) << 16);
-        delay[k] = ld(s.tr_delay, ix(hk));
+        pos[k] = ld(s.tr_pos, tix(hk));
+        bits[k] = ld(s.tr_bits, tix(hk));
+        plan[k] = ld(s.tr_plan, tix(hk));
+        nprv[k] = (uint32_t)ld(s.tr_next, tix(hk)) | ((uint32_t)ld(s.tr_prev, tix(hk)) << 16);
+        sdec[k] = (uint32_t)ld(s.tr_src, tix(hk)) | ((uint32_t)ld(s.tr_dec, tix(hk)) << 16);
+        delay[k] = ld(s.tr_delay, tix(hk));
         *(vec_t<int32_t, 4>*)(ltt + 8 * hk) = ld((const vec_t<int32_t, 4>*)m.tr_pack, (size_t)hk * 2u);
         *(vec_t<int32_t, 4>*)(ltt + 8 * hk + 4) = ld((const vec_t<int32_t, 4>*)m.tr_pack, (size_t)hk * 2u + 1u);
       } else {
@@ -503,12 +515,12 @@ struct WEnv {
 #pragma unroll
     for (int k = 0; k < PPL; ++k) {
       const int p = k * 64 + lane;
-      sem(k) = p < m.NP ? r_from64(ld(s.sem, ix(p))) : 0u;
+      sem(k) = p < m.NP ? r_from64(ld(s.sem, pix(p))) : 0u;
     }
 #pragma unroll
     for (int k = 0; k < SPL; ++k) {
       const int sw = k * 64 + lane;
-      lcnt[k * 64 + lane] = sw < m.S ? ld(s.counts, ix(sw)) : 0u;
+      lcnt[k * 64 + lane] = sw < m.S ? ld(s.counts, cix(sw)) : 0u;
     }
     now = uni(ld(s.elapsed, e));
     flags = uni(ld(s.eflags, e));
@@ -539,29 +551,29 @@ struct WEnv {
     for (int k = 0; k < TPL; ++k) {
       const int hk = lane + 64 * k;
       if (mine[k]) {
-        st(s.tr_pos, ix(hk), pos[k]);
-        st(s.tr_bits, ix(hk), bits[k]);
-        st(s.tr_plan, ix(hk), plan[k]);
-        st(s.tr_next, ix(hk), (uint16_t)(nprv[k] & 0xFFFFu));
-        st(s.tr_prev, ix(hk), (uint16_t)(nprv[k] >> 16));
-        st(s.tr_src, ix(hk), (uint16_t)(sdec[k] & 0xFFFFu));
-        st(s.tr_dec, ix(hk), (uint16_t)(sdec[k] >> 16));
-        st(s.tr_delay, ix(hk), delay[k]);
+        st(s.tr_pos, tix(hk), pos[k]);
+        st(s.tr_bits, tix(hk), bits[k]);
+        st(s.tr_plan, tix(hk), plan[k]);
+        st(s.tr_next, tix(hk), (uint16_t)(nprv[k] & 0xFFFFu));
+        st(s.tr_prev, tix(hk), (uint16_t)(nprv[k] >> 16));
+        st(s.tr_src, tix(hk), (uint16_t)(sdec[k] & 0xFFFFu));
+        st(s.tr_dec, tix(hk), (uint16_t)(sdec[k] >> 16));
+        st(s.tr_delay, tix(hk), delay[k]);
       }
     }
 #pragma unroll
     for (int k = 0; k < PPL; ++k) {
       const int p = k * 64 + lane;
-      if (p < m.NP) st(s.sem, ix(p), r_to64(sem(k)));
+      if (p < m.NP) st(s.sem, pix(p), r_to64(sem(k)));
     }
 #pragma unroll
     for (int k = 0; k < SPL; ++k) {
       const int sw = k * 64 + lane;
-      if (sw < m.S) st(s.counts, ix(sw), lcnt[k * 64 + lane]);
+      if (sw < m.S) st(s.counts, cix(sw), lcnt[k * 64 + lane]);
     }
     uint32_t err = 0;
 #pragma unroll
-    for (int b = 0; b < 4; ++b)
+    for (int b = 0; b < (PART ? 5 : 4); ++b)
       if (__ballot((lerr >> b) & 1u)) err |= 1u << b;
     if (lane == 0) {
       st(s.phase, e, phase);
@@ -1056,11 +1068,15 @@ struct WEnv {
     const bool row_ok = pos[ks] >= 0 && dd < DIST_INF && (pin >> 2) == sw && slot < np;
     const uint32_t qoff = pp[3] + ((pend >> 14) & 0x3FFFu) * (pp[1] >> 16) + ((pend >> 28) & 3u);
     // level 3: Q values
-    const double* rp = qbase() + (row_ok ? roff : 0u);
-    double rv[4];
+    // (PART: the rows live on their owners; nothing is staged)
+    double rv[4] = {0.0, 0.0, 0.0, 0.0};
+    double qv = 0.0;
+    if constexpr (!PART) {
+      const double* rp = qbase() + (row_ok ? roff : 0u);
 #pragma unroll
-    for (int c = 0; c < 4; ++c) rv[c] = ld(rp, (size_t)((uint32_t)c < w ? c : 0));
-    const double qv = ld(qbase(), (size_t)(hp ? qoff : 0u));
+      for (int c = 0; c < 4; ++c) rv[c] = ld(rp, (size_t)((uint32_t)c < w ? c : 0));
+      qv = ld(qbase(), (size_t)(hp ? qoff : 0u));
+    }
 #pragma unroll
     for (int c = 0; c < 4; ++c) pfl[c] = rv[c];
     // the greedy choice on the staged row (distr_q.py:449-490, as in decide): valid whenever the
@@ -1098,8 +1114,8 @@ struct WEnv {
     }
     pfl[4] = qv;
     pfl[5] = __longlong_as_double((long long)slw);
-    pf_roff[ks] = row_ok ? roff : PF_NONE;
-    pf_qoff[ks] = hp ? qoff : PF_NONE;
+    pf_roff[ks] = (row_ok && !PART) ? roff : PF_NONE;
+    pf_qoff[ks] = (hp && !PART) ? qoff : PF_NONE;
   }
   // a Q cell of this env was written (uniform offset): drop staged copies that contain it
   __device__ __forceinline__ void pf_written(uint32_t off) {
@@ -1128,7 +1144,11 @@ struct WEnv {
     uint32_t abytes;    // algorithmic bytes of the decision
   };
 
-  __device__ __forceinline__ void decide(Dec& d, bool greedy) {
+  // PART: true = observe pass (no reply yet): the request went to the row's owner and nothing of
+  // the env changed (the next launch repeats the observation, which is deterministic, and
+  // applies the reply)
+  __device__ __forceinline__ bool decide(Dec& d, bool greedy) {
+    const bool observe_only = PART && !(flags & F_REQ);
     SFL_PT(t_obs);
     SFL_LAP0();
     // agent_iter: lowest queued train (switch_env.py:418-421, 616-622)
@@ -1140,7 +1160,7 @@ struct WEnv {
     SFL_LAP(0);
     SFL_PCNT(8);
     const int h = mctz(q_mask);
-    mclear_low(q_mask);
+    if (!observe_only) mclear_low(q_mask);
     const uint32_t sd = trl(sdec, h);
     const int sw = (int)(sd >> 16);
     const SwRec swr = sw_rec(sw);
@@ -1210,7 +1230,7 @@ struct WEnv {
     double v_c = 0.0;
     if (row_hit) {
       SFL_PCNT(4);
-    } else {
+    } else if (!PART) {
       v_c = ld(qbase() + roff, (size_t)(colv ? lane : 0));
       SFL_PCNT(5);
     }
@@ -1227,7 +1247,9 @@ struct WEnv {
       const PortRec pr = port_rec(4 * ps + pslot);
       d.qoff_pend = pr.q_off() + pstate * (uint32_t)pr.q_w() + (uint32_t)pj;
       d.row_pend = pr.row_base() + pstate;
-      if (pf_qoff_h == d.qoff_pend) {
+      if (PART) {
+        // the pending update is applied by its row's owner
+      } else if (pf_qoff_h == d.qoff_pend) {
         q_pend_v = pf_qp;
         SFL_PCNT(6);
       } else {
@@ -1253,8 +1275,8 @@ struct WEnv {
       const uint32_t n = n_sw;
       // eps0 * decay**n (distr_q.py:59-68): host-computed table (a scalar load, K$-resident), pow beyond it
       const double eps = n < (uint32_t)m.ntab ? ldc(m.eps_tab, (size_t)n) : m.eps0 * pow_ool(m.eps_decay, (double)n);
-      if (unid(pcg_double(rng)) < eps) {
-        explore = true;
+      explore = unid(pcg_double(rng)) < eps;
+      if (explore && !observe_only) {
         const uint32_t sub_seed = pcg_bounded(rng, 2147483646u);
         const uint32_t nvalid = (uint32_t)__builtin_popcount(amask);
         // Discrete.sample(mask) == valid[default_rng(sub_seed).integers(0, nvalid)]: Lemire on the
@@ -1279,11 +1301,19 @@ struct WEnv {
                              (uint32_t)__builtin_popcount(amask & ((1u << la16) - 1u)) == pick;
         action = ctz64(__ballot(is_pick));
       }
-      {  // uniform values, written by every lane
+      if (!observe_only) {  // uniform values, written by every lane
         lrng[0] = rng.shi;
         lrng[1] = rng.slo;
         lrng[4] = ((uint64_t)rng.has << 32) | rng.buf;
       }
+    }
+    if constexpr (PART) {
+      if (observe_only) {
+        emit_req(sw, slot, state, amask, explore);
+        flags |= F_REQ;
+        return true;
+      }
+      flags &= ~F_REQ;
     }
     SFL_LAP(6);
     d.q_pend = unid(q_pend_v);
@@ -1293,7 +1323,14 @@ struct WEnv {
     // action a(c); every other action of the full row is default_q, the first of them at mind
     double mx;
     int best, arg;
-    if (row_hit) {
+    if constexpr (PART) {
+      // the owner's reply: max over the full row, and the masked argmax (-1 for an exploratory request)
+      const uint32_t ix = uni(ld(P->req_ix, (size_t)e));
+      const vec_t<int32_t, 4> rw =
+          ld((const vec_t<int32_t, 4>*)(P->rep_in + (size_t)(ix >> 24) * (P->cap_req + 1) + (ix & 0xFFFFFFu)), 0);
+      best = arg = uni(rw[0]);
+      mx = __longlong_as_double(((long long)(uint32_t)uni(rw[3]) << 32) | (long long)(uint32_t)uni(rw[2]));
+    } else if (row_hit) {
       mx = unid(pf_mx);
       const uint32_t ba = uni((uint32_t)pfd67[0]);
       best = (int)(ba & 0xFFu);
@@ -1423,14 +1460,63 @@ struct WEnv {
     d.abytes = 220u + 48u * (uint32_t)np + 8u * (uint32_t)na;  // SURVEY.md §8(d) bytes of this decision
     SFL_LAP(9);
     SFL_PACC(2, t_ap);
+    return false;
+  }
+
+  // ---- graph-partitioned mode: messages to the owners (sfl_part.h records) ---------------------
+  // lane 0: the decision's row request (the row's owner answers max(row) and the masked argmax)
+  __device__ __forceinline__ void emit_req(int sw, int slot, uint32_t state, uint32_t amask, bool explore) {
+    if (lane != 0) return;
+    const int dst = ld(P->owner, (size_t)sw);
+    const uint32_t k = atomicAdd(P->cnt + dst, 1u);
+    if (k >= P->cap_req) {
+      lerr |= E_MSG_OVF;
+      return;
+    }
+    u4 r;
+    r[0] = P->env_base + e;
+    r[1] = (uint32_t)(4 * sw + slot) | (amask << 16);
+    r[2] = state;
+    r[3] = explore ? 1u : 0u;
+    static_assert(sizeof(PartReq) == sizeof(u4), "request record");
+    st((u4*)P->req_out, (size_t)dst * (P->cap_req + 1) + 1 + k, r);
+    st(P->req_ix, (size_t)e, ((uint32_t)dst << 24) | (1u + k));
+  }
+  // any lane: one update record (kind 0: q <- (1 - lr) q + lr target, and the key-set insert;
+  // kind 1: the key-set insert only) to the owner of switch sw, applied in stage order
+  __device__ __forceinline__ void emit_upd(int sw, int slot, uint32_t state, int j, uint32_t kind, double lr, double target,
+                                           int stage) {
+    const int dst = ld(P->owner, (size_t)sw);
+    const uint32_t k = atomicAdd(P->cnt + P->world + dst, 1u);
+    if (k >= P->cap_upd) {
+      lerr |= E_MSG_OVF;
+      return;
+    }
+    u4 a, b;
+    a[0] = P->env_base + e;
+    a[1] = (uint32_t)(4 * sw + slot) | ((uint32_t)j << 16) | ((uint32_t)stage << 24);
+    a[2] = state;
+    a[3] = kind;
+    b[0] = (uint32_t)__double_as_longlong(lr);
+    b[1] = (uint32_t)(__double_as_longlong(lr) >> 32);
+    b[2] = (uint32_t)__double_as_longlong(target);
+    b[3] = (uint32_t)(__double_as_longlong(target) >> 32);
+    static_assert(sizeof(PartUpd) == 2 * sizeof(u4), "update record");
+    u4* u = (u4*)(P->upd_out + (size_t)dst * (P->cap_upd + 1) + 1 + k);
+    st(u, 0, a);
+    st(u, 1, b);
+    if (stage > 0) atomicMax(P->max_stage, (uint32_t)stage);
   }
 
   // ---- post-step part of the learn loop (distr_q.py:322-362) -----------------------------------
   // The (switch, train) slot of the deciding switch is consumed and the successor slot gets
   // the new pending update and the reward the train will see there (AECEnv.last).
   __device__ __forceinline__ void post(const Dec& d, bool greedy) {
+    if constexpr (PART) {
+      post_part(d, greedy);
+      return;
+    }
     SFL_LAP0();
-    const int T = m.T;
     if (greedy) {
       if (lane == 0) {
         if (d.touch_cur) touch_row(d.row_cur);
@@ -1501,6 +1587,52 @@ struct WEnv {
     cset(d.sw, cget(d.sw) + 1u);
     SFL_LAP(10);
   }
+  // PART: post with the Q operations as update records to the rows' owners (env_post with MsgQ
+  // in sfl_part.h; stage 0 = the pending update, 1 + i = the bonus of the i-th arrived train);
+  // the decision row's key-set insert was done by its owner when it answered a greedy request
+  __device__ __forceinline__ void post_part(const Dec& d, bool greedy) {
+    if (greedy) {
+      if (lane == 0) st(slotb, slot_ix(d.next_sw, d.h), slot_make(PEND_NONE, d.r_new, epoch));
+      return;
+    }
+    const uint32_t pend = slot_pend(d.slotword, epoch);
+    const bool hp = pend != PEND_NONE;
+    const int ps = hp ? (int)(pend & 0xFFFu) : 0;
+    const double lr = lr_of(cget(ps));
+    if (lane == 0) {
+      if (hp) {
+        const double r = (double)d.reward;
+        const double target = d.sw != ps ? r + m.gamma * d.mq : r;
+        emit_upd(ps, (int)((pend >> 12) & 3u), (pend >> 14) & 0x3FFFu, (int)((pend >> 28) & 3u), 0u, lr, target, 0);
+        if (d.sw != ps && !d.touch_cur) emit_upd(d.sw, d.slot, d.state, 0, 1u, 0.0, 0.0, 0);
+      }
+      st(slotb, slot_ix(d.sw, d.h), slot_make(PEND_NONE, slot_rew(d.slotword, epoch), epoch));
+      st(slotb, slot_ix(d.next_sw, d.h),
+         slot_make(pend_make((uint32_t)d.sw, (uint32_t)d.slot, d.state, (uint32_t)d.j), d.r_new, epoch));
+    }
+    Mask fresh = arr_mask & ~fl_mask;
+    fl_mask |= fresh;
+    if (many(fresh)) pf_ok = false;
+    int stage = 1;
+    while (many(fresh)) {
+      const int tr = mctz(fresh);
+      mclear_low(fresh);
+      for (int base = 0; base < m.S; base += 64) {
+        const int sw2 = base + lane;
+        const bool valid = sw2 < m.S;
+        const uint64_t slw = valid ? ld(slotb, slot_ix(sw2, tr)) : 0ull;
+        const uint32_t pe = valid ? slot_pend(slw, epoch) : PEND_NONE;
+        const int ps2 = pe == PEND_NONE ? 0 : (int)(pe & 0xFFFu);
+        const uint32_t n = cget_var(ps2);  // all lanes active: a bpermute reads 0 from inactive lanes
+        if (pe == PEND_NONE) continue;
+        emit_upd(ps2, (int)((pe >> 12) & 3u), (pe >> 14) & 0x3FFFu, (int)((pe >> 28) & 3u), 0u, lr_of_var(n),
+                 1000.0 + m.gamma * 0.0, stage);
+        st(slotb, slot_ix(sw2, tr), slot_make(PEND_NONE, slot_rew(slw, epoch), epoch));
+      }
+      ++stage;
+    }
+    cset(d.sw, cget(d.sw) + 1u);
+  }
 
   // order-independent checksum of the semaphore table (trace/debug only)
   __device__ __forceinline__ uint64_t sem_checksum() const {
@@ -1518,17 +1650,21 @@ struct WEnv {
 // driver: one env per wavefront until its episode target / decision budget (env_run in sfl_core.h)
 // TRACE: the per-decision trace of one env (parity tests only) is compiled into a separate
 // instantiation, so the production kernel does not carry its registers
-template <int PPL, int SPL, int TW, bool TRACE>
-__device__ void run(const SflMap& m, const SflState& s, const SflCtl& c) {
-  using V = WEnv<PPL, SPL, TW>;
+// PART: one round of the graph-partitioned mode (P = its tables and this round's message
+// buffers): each env applies the reply to its open request, runs to its next decision and stops
+// after emitting that decision's request; c.dec_budget counts decisions since sfl_part_begin
+template <int PPL, int SPL, int TW, bool TRACE, bool PART = false>
+__device__ void run(const SflMap& m, const SflState& s, const SflCtl& c, const SflPart* P = nullptr) {
+  using V = WEnv<PPL, SPL, TW, PART>;
   constexpr int LDS_WORDS = 64 * (PPL + SPL) + TW * PF_W * 2 + 12 + TW * 8;  // semaphores, counters, prefetch records, rng, timetable
   const int lane = (int)__lane_id();
   const uint32_t e = uni((uint32_t)((blockIdx.x * blockDim.x + threadIdx.x) >> 6));
   if (e >= s.E) return;
   constexpr int WPB = TW > 64 ? 1 : SFL_WAVE_BLOCK / 64;  // waves (envs) per block (sfl.hip launches)
   __shared__ uint32_t lds[WPB * LDS_WORDS];
-  V v(m, s, e, lane, lds + (threadIdx.x >> 6) * LDS_WORDS);
+  V v(m, s, e, lane, lds + (threadIdx.x >> 6) * LDS_WORDS, P);
   v.load();
+  const int64_t dec_base = PART ? (int64_t)uni((uint64_t)ld(P->dec_done, e)) : 0;
   int32_t phase = uni(ld(s.phase, e));
   int32_t ep_t = uni(ld(s.ep_t, e)), n_test = uni(ld(s.n_test, e));
   uint32_t ticks = 0, abytes = 0;
@@ -1600,7 +1736,7 @@ __device__ void run(const SflMap& m, const SflState& s, const SflCtl& c) {
         v.step_ctr += 1;
         if (v.step_ctr > max_steps) v.flags |= F_TRUNC;
         phase = (v.flags & (F_TERM | F_TRUNC)) ? PH_END : PH_DECIDE;
-        return dec_budget > 0 && (int64_t)v.n_dec >= dec_budget;
+        return dec_budget > 0 && dec_base + (int64_t)v.n_dec >= dec_budget;
       };
       // a batch of queued decisions: decide, and post each one while more are queued (the last
       // one is posted after the ticks that follow it, switch_env.py:418-421 / distr_q.py:322-343);
@@ -1608,9 +1744,17 @@ __device__ void run(const SflMap& m, const SflState& s, const SflCtl& c) {
       bool stop = false, do_decide = phase == PH_DECIDE;
       while (true) {
         if (do_decide) {
+          if (PART && !(v.flags & F_REQ) && dec_budget > 0 && dec_base + (int64_t)v.n_dec >= dec_budget) {
+            stop = true;  // this part step's decisions are done: no new request
+            break;
+          }
           SFL_PT(t0);
-          v.decide(d, greedy);
+          const bool requested = v.decide(d, greedy);
           SFL_PACC(2, t0);
+          if (PART && requested) {
+            stop = true;  // the round ends at the request (phase stays PH_DECIDE)
+            break;
+          }
           abytes += d.abytes;
           v.flags |= F_INFLIGHT;
           if (!many(v.q_mask)) {
@@ -1666,6 +1810,7 @@ __device__ void run(const SflMap& m, const SflState& s, const SflCtl& c) {
   }
 #endif
   if (lane == 0) {
+    if (PART) st(P->dec_done, e, dec_base + (int64_t)v.n_dec);
     st(s.ep_t, e, ep_t);
     st(s.n_test, e, n_test);
     if (c.launch_dec) st(c.launch_dec, e, (uint64_t)v.n_dec);
