@@ -465,7 +465,8 @@ int check_errors(Handle<B>* h) {
   for (uint32_t e = 0; e < h->E; ++e)
     if (err[e]) {
       char buf[160];
-      snprintf(buf, sizeof buf, "env %u: error flags 0x%x (1=inf distance, 2=plan overflow, 4=port mismatch, 8=bad action)",
+      snprintf(buf, sizeof buf, "env %u: error flags 0x%x (1=inf distance, 2=plan overflow, 4=port mismatch, 8=bad action, "
+               "16=message segment overflow)",
                e, err[e]);
       return fail(buf);
     }

@@ -99,9 +99,16 @@ class PartitionedBatch:
         nrep = self.world * (self.cap_req + 1) * rp.value
         nupd = self.world * (self.cap_upd + 1) * up.value
         z = lambda n: torch.zeros(n, dtype=torch.uint8, device=dev)  # noqa: E731
-        self.req_send, self.req_recv = z(nreq), z(nreq)
-        self.rep_send, self.rep_recv = z(nrep), z(nrep)
-        self.upd_send, self.upd_recv = z(nupd), z(nupd)
+        if self.world == 1:
+            # one rank: every segment is addressed to this rank, so the exchange is the identity
+            # and each receive buffer is its send buffer (no copies, no stream synchronisation)
+            self.req_send = self.req_recv = z(nreq)
+            self.rep_send = self.rep_recv = z(nrep)
+            self.upd_send = self.upd_recv = z(nupd)
+        else:
+            self.req_send, self.req_recv = z(nreq), z(nreq)
+            self.rep_send, self.rep_recv = z(nrep), z(nrep)
+            self.upd_send, self.upd_recv = z(nupd), z(nupd)
         self.on_gpu = dev.type == "cuda"
         self.rounds = 0
 
@@ -117,6 +124,8 @@ class PartitionedBatch:
 
     # ---- one part step: every env makes `decisions_per_env` decisions ---------------------------
     def _exchange(self, recv, send):
+        if recv is send:
+            return
         if self.dist is None or self.world == 1:
             recv.copy_(send)
         elif recv.is_cuda and self.dist.get_backend() == "gloo":
