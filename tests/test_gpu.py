@@ -172,6 +172,15 @@ def test_partitioned_rounds_gpu_equal_fused(lib, cfg, E, kernel):
     ref.close()
 
 
+@pytest.mark.parametrize("cfg", ["c2", "c5"])
+def test_two_rank_partition_wave_gpu(lib, cfg):
+    """Two ranks (processes) on GPU 0 over gloo: k_wave's PART local step with the row requests,
+    replies and update records crossing ranks; each rank's owned Q rows, key set and env states
+    bit-equal to the fused run of all envs (host build)."""
+    from tests import test_partition
+    test_partition.two_rank_run(cfg, gpu=True)
+
+
 @pytest.mark.parametrize("S,T,variant", [(64, 48, 3), (100, 48, 4), (120, 64, 4), (100, 100, 5), (200, 40, 5),
                                          (256, 128, 5)])
 def test_wave_kernel_shapes(lib, S, T, variant):
