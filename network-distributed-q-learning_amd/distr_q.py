@@ -81,8 +81,11 @@ class DistrQLearning:
         mfs = np.zeros((num_episodes, E), np.int32)
         cum_x = np.zeros((num_episodes, E))
         arr_x = np.zeros((num_episodes, E), np.int32)
-        # checkpoints are written at the start of episode t with (t+1) % checkpoint_freq == 0
+        # checkpoints are written at the start of episode t with (t+1) % checkpoint_freq == 0, after
+        # that episode's exploit round (distr_q.py:278-294): when both fall on t, the greedy round
+        # runs here (its max_action key-set inserts belong in the checkpoint) and the kernel skips it
         stops = [t for t in range(num_episodes) if checkpoint_freq and (t + 1) % checkpoint_freq == 0]
+        pre_x = {}
         done = 0
         for stop in stops + [num_episodes]:
             n = stop - done
@@ -97,6 +100,10 @@ class DistrQLearning:
                 done = stop
             if stop < num_episodes:
                 t = stop
+                if f and (t + 1) % f == 0 and not (t == 0 and pre is not None):
+                    x = b.test(1)
+                    b.lib.check(b.lib.dll.sfl_mark_exploit_done(b.h), "sfl_mark_exploit_done")
+                    pre_x[t] = (x["cum_reward"][0], x["arrived"][0])
                 self.save(os.path.join(out_dir, f"checkpoint_{t + 1}.pkl"))
                 self._save(out_dir, f"cum_reward_checkpoint_{t + 1}.npz", self._env_major(cum))
                 self._save(out_dir, f"arrived_trains_checkpoint_{t + 1}.npz", self._env_major(arrived[:t]))
@@ -107,6 +114,9 @@ class DistrQLearning:
         if pre is not None:
             cum_x[0] = pre["cum_reward"][0]
             arr_x[0] = pre["arrived"][0]
+        for t, (c_, a_) in pre_x.items():  # (the kernel's rows for these episodes were not written)
+            cum_x[t] = c_
+            arr_x[t] = a_
         self._save(out_dir, "cum_reward.npz", self._env_major(cum))
         self._save(out_dir, "arrived_trains.npz", self._env_major(arrived))
         self._save(out_dir, "delays.npz", self._env_major(delays, delays=True))

@@ -807,19 +807,24 @@ class OracleDistrQ:
         delays = [v[1] for v in env.last_node.values()]
         return cum, len(post["arrived_trains"]), delays
 
-    def learn(self, num_episodes, exploit_freq=None):
-        """distr_q.py:244-379; returns the arrays the reference writes as .npz."""
+    def learn(self, num_episodes, exploit_freq=None, checkpoint_freq=None):
+        """distr_q.py:244-379; returns the arrays the reference writes as .npz.  With checkpoint_freq,
+        out["checkpoints"][t + 1] is the Q dict the reference pickles at distr_q.py:288-289 -- after
+        that episode's exploit round (278-281), before its reset."""
         env = self.env
         cum = np.zeros(num_episodes)
         arrived, delays, mfs, cum_x, arr_x = [], [], [], [], []
         counts = {a: 0 for a in env.agents}
         rng = np.random.default_rng(self.seed)
         post = None
+        ckpt = {}
         for t in range(num_episodes):
             if exploit_freq is not None and (t + 1) % exploit_freq == 0:
                 tr_, ta_, _ = self.test()
                 cum_x.append(tr_)
                 arr_x.append(ta_)
+            if checkpoint_freq and (t + 1) % checkpoint_freq == 0:
+                ckpt[t + 1] = {k: list(v) for k, v in self.q.items()}
             pending: Dict[tuple, tuple] = {}
             at_dest: List[int] = []
             if self.trace:
@@ -869,6 +874,8 @@ class OracleDistrQ:
         if exploit_freq is not None:
             out["cum_reward_exploit"] = cum_x
             out["arrived_trains_exploit"] = arr_x
+        if checkpoint_freq:
+            out["checkpoints"] = ckpt
         return out
 
 

@@ -59,3 +59,29 @@ def test_batch_outputs_have_env_axis(tmp_path):
     assert cr.shape == (3, 4)
     assert cr[0].tolist() == g["learn"]["outputs"]["cum_reward"][:4]
     assert _load(tmp_path, "delays").shape == (3, 4, env.compiled.T)
+
+
+@pytest.mark.parametrize("name", ["c2_s3", "city6_s5"])
+def test_checkpoint_after_coinciding_exploit_round(tmp_path, name):
+    """distr_q.py:278-294: when an exploit round and a checkpoint fall on the same episode, the
+    exploit round (test(), whose max_action inserts keys) runs first and the checkpoint pickles the
+    Q dict after it.  Checked against the oracle's snapshots at the same points."""
+    from oracle import sfl_oracle as so
+    g = _golden.load(name)
+    hp = g["hparams"]
+    f = g["exploit_freq"]
+    n = 3 * f + 1
+    env = envmod.ASyncSwitchEnv(g["scenario_obj"], max_steps=100_000)
+    model = dq.DistrQLearning(env, seed=g["seed"], lib=hostsim.lib(), **{k: hp[k] for k in
+                              ("gamma", "epsilon", "epsilon_decay_rate", "lr", "lr_decay_rate", "default_q")})
+    model.learn(n, str(tmp_path), checkpoint_freq=f, exploit_freq=f)
+    _, om = so.build(g["scenario_obj"], g["seed"], hp, trace=False)
+    ref = om.learn(n, exploit_freq=f, checkpoint_freq=f)
+    assert sorted(ref["checkpoints"]) == [f, 2 * f, 3 * f]
+    for t1, q in ref["checkpoints"].items():
+        with open(tmp_path / f"checkpoint_{t1}.pkl", "rb") as fh:
+            assert pickle.load(fh) == q, t1
+    assert _load(tmp_path, "cum_reward").tolist() == ref["cum_reward"]
+    assert _load(tmp_path, "cum_reward_exploit").tolist() == ref["cum_reward_exploit"]
+    assert _load(tmp_path, "arrived_trains_exploit").tolist() == ref["arrived_trains_exploit"]
+    assert model.q_table == om.q
