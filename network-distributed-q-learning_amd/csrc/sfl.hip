@@ -227,6 +227,23 @@ struct HipBackend {
     k_qinit<<<blocks, 256, 0, stream>>>(m, s, n_rows, port, state, vals);
     check(hipGetLastError(), "k_qinit");
   }
+#ifdef SFL_PROFILE
+  // tuning builds: the wave kernels' phase cycles (sfl_wave.h g_prof), printed and cleared
+  void print_prof() {
+      unsigned long long pr[32] = {};
+      hipMemcpyFromSymbol(pr, HIP_SYMBOL(sfl::wave::g_prof), sizeof pr);
+      fprintf(stderr,
+              "[sfl profile] cycles reset %.3e tick %.3e decide %.3e (observe %.3e egreedy %.3e apply %.3e) post %.3e "
+              "total %.3e | prefetch %llu row hit %llu miss %llu pend hit %llu miss %llu decisions %llu\n",
+              (double)pr[0], (double)pr[1], (double)pr[2], (double)pr[5], (double)pr[6], (double)pr[7], (double)pr[3],
+              (double)pr[4], pr[8], pr[9], pr[10], pr[11], pr[12], pr[13]);
+      fprintf(stderr, "[sfl laps]");
+      for (int k = 0; k < 16; ++k) fprintf(stderr, " %d:%.3e", k, (double)pr[16 + k]);
+      fprintf(stderr, "\n");
+      unsigned long long z[32] = {};
+      hipMemcpyToSymbol(HIP_SYMBOL(sfl::wave::g_prof), z, sizeof z);
+    }
+#endif
   int run(const sfl::SflMap& m, const sfl::SflState& s, const sfl::SflCtl& c, int variant, float* ms) {
     static_assert(sizeof(sfl::SflMap) + sizeof(sfl::SflState) + sizeof(sfl::SflCtl) + 64 < 4096, "params");
     const unsigned blocks = (s.E + 255) / 256;
@@ -274,20 +291,7 @@ struct HipBackend {
     hipEventElapsedTime(&t, ev0, ev1);
     *ms = t;
 #ifdef SFL_PROFILE
-    if (variant > 0) {
-      unsigned long long pr[32] = {};
-      hipMemcpyFromSymbol(pr, HIP_SYMBOL(sfl::wave::g_prof), sizeof pr);
-      fprintf(stderr,
-              "[sfl profile] cycles reset %.3e tick %.3e decide %.3e (observe %.3e egreedy %.3e apply %.3e) post %.3e "
-              "total %.3e | prefetch %llu row hit %llu miss %llu pend hit %llu miss %llu decisions %llu\n",
-              (double)pr[0], (double)pr[1], (double)pr[2], (double)pr[5], (double)pr[6], (double)pr[7], (double)pr[3],
-              (double)pr[4], pr[8], pr[9], pr[10], pr[11], pr[12], pr[13]);
-      fprintf(stderr, "[sfl laps]");
-      for (int k = 0; k < 16; ++k) fprintf(stderr, " %d:%.3e", k, (double)pr[16 + k]);
-      fprintf(stderr, "\n");
-      unsigned long long z[32] = {};
-      hipMemcpyToSymbol(HIP_SYMBOL(sfl::wave::g_prof), z, sizeof z);
-    }
+    if (variant > 0) print_prof();
 #endif
     return err.empty() ? 0 : -1;
   }
@@ -378,6 +382,9 @@ struct HipBackend {
     check(hipEventRecord(ev1, stream), "event");
     if (!check(hipEventSynchronize(ev1), "k_part_local")) return -1;
     hipEventElapsedTime(ms, ev0, ev1);
+#ifdef SFL_PROFILE
+    if (variant > 0) print_prof();
+#endif
     return err.empty() ? 0 : -1;
   }
   void part_answer(const sfl::SflMap& m, const sfl::SflPart& P, const sfl::PartReq* in, sfl::PartRep* out) {

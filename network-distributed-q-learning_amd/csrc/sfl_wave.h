@@ -1152,7 +1152,9 @@ struct WEnv {
     SFL_PT(t_obs);
     SFL_LAP0();
     // agent_iter: lowest queued train (switch_env.py:418-421, 616-622)
-    if (!pf_ok) {
+    // (PART observe pass: the observation needs one distance, looked up directly below; the
+    // staging waits for the apply pass in the next launch)
+    if (!pf_ok && !observe_only) {
       prefetch(greedy);
       pf_ok = true;
       SFL_PCNT(3);
@@ -1208,7 +1210,8 @@ struct WEnv {
     const uint32_t b = trl(bits, h);
     const int32_t p0 = trl(pos, h);
     const int32_t ed = tr[0], la = tr[1], k = tr[2];
-    const int32_t dl = now - la + dist_staged(uni(pfd01[0]));
+    const int32_t d_obs = observe_only ? dist(k, p0, (int)tb_dir(b)) : dist_staged(uni(pfd01[0]));
+    const int32_t dl = now - la + d_obs;
     const int32_t avail = la - ed;
     const uint32_t lvl = dl <= 0 ? 0u : (dl <= avail * 20 ? 1u : 2u);
     const uint32_t state = ((free_bits * (uint32_t)m.K) + (uint32_t)k) * 3u + lvl;
@@ -1239,7 +1242,7 @@ struct WEnv {
     const uint32_t pend = greedy ? PEND_NONE : slot_pend(d.slotword, epoch);
     d.qoff_pend = PF_NONE;
     double q_pend_v = 0.0;
-    if (pend != PEND_NONE) {
+    if (!observe_only && pend != PEND_NONE) {  // (observe pass: the LDS record was not staged)
       const int ps = (int)(pend & 0xFFFu);
       const int pslot = (int)((pend >> 12) & 3u);
       const uint32_t pstate = (pend >> 14) & 0x3FFFu;
