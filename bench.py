@@ -107,7 +107,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--partition", action="store_true",
                     help="graph-partitioned mode (BASELINE configs[4]): switch agents owned by ranks, RCCL all-to-all "
-                         "of row lookups and updates; defaults to --config c5 --envs 8192")
+                         "of row lookups and updates; defaults to --config c5 --envs 16384 (238 GB of owned Q rows per GPU)")
     args = ap.parse_args()
     if args.partition:
         return bench_partition(args)
@@ -208,7 +208,7 @@ def bench_partition(args):
     mapgen = importlib.import_module(PKG + ".mapgen")
     comp = importlib.import_module(PKG + ".compiler")
     cfg = args.config if args.config != "c3" else "c5"
-    E = args.envs if args.envs != 65536 else 8192
+    E = args.envs if args.envs != 65536 else 16384
     cm = comp.compile_scenario(mapgen.make_config(cfg))
     seeds = par.shard_seeds(450565, E, rank)
     pb = part.PartitionedBatch(cm, HP, seeds, rank * E, world * E, rank=rank, world=world, dist=dist, device=dev,
