@@ -216,6 +216,14 @@ struct HipBackend {
     check(hipStreamSynchronize(stream), "d2h sync");
   }
   void memset(void* p, int v, size_t n) { check(hipMemsetAsync(p, v, n, stream), "memset"); }
+  // stream-ordered copy without the synchronisation (the caller syncs once for several)
+  void d2h_async(void* d, const void* s, size_t n) { check(hipMemcpyAsync(d, s, n, hipMemcpyDeviceToHost, stream), "d2h"); }
+  // time between the events of the last launch (after a sync)
+  float elapsed_ms() {
+    float t = 0.f;
+    hipEventElapsedTime(&t, ev0, ev1);
+    return t;
+  }
   void fill_f64(double* p, double v, size_t n) {
     k_fill_f64<<<4096, 256, 0, stream>>>(p, v, n);
     check(hipGetLastError(), "k_fill_f64");
@@ -380,9 +388,11 @@ struct HipBackend {
     if (!check(hipGetLastError(), "k_part_local")) return -1;
     k_part_headers<<<1, 256, 0, stream>>>(&pp->P);
     check(hipEventRecord(ev1, stream), "event");
-    if (!check(hipEventSynchronize(ev1), "k_part_local")) return -1;
-    hipEventElapsedTime(ms, ev0, ev1);
+    // (no synchronisation here: the caller issues the launch totals and the count copies behind
+    // it and syncs once; *ms is read with elapsed_ms() after that)
+    *ms = 0.f;
 #ifdef SFL_PROFILE
+    if (!check(hipEventSynchronize(ev1), "k_part_local")) return -1;
     if (variant > 0) print_prof();
 #endif
     return err.empty() ? 0 : -1;

@@ -455,9 +455,9 @@ int reduce_launch(Handle<B>* h) {
   return 0;
 }
 
+// the per-env error flags, when the launch totals reported any (h->last_err)
 template <class B>
-int check_errors(Handle<B>* h) {
-  if (int rc = reduce_launch(h)) return rc;
+int scan_errors(Handle<B>* h) {
   if (!h->last_err) return 0;
   std::vector<uint32_t> err(h->E);
   h->be.d2h(err.data(), h->st.err, h->E * 4);
@@ -471,6 +471,12 @@ int check_errors(Handle<B>* h) {
       return fail(buf);
     }
   return 0;
+}
+
+template <class B>
+int check_errors(Handle<B>* h) {
+  if (int rc = reduce_launch(h)) return rc;
+  return scan_errors(h);
 }
 
 template <class B>
@@ -720,15 +726,26 @@ int part_local(Handle<B>* h, int64_t budget, const void* rep_in, void* req_out, 
   c.launch_bytes = h->d_launch_bytes;
   float ms = 0.f;
   int rc = h->be.part_local(h->map, h->st, c, P, h->variant, &ms);
-  h->last_kernel_ms = ms;
+  // the launch totals, the record counts and the totals' copy queued behind the kernels: one sync
   std::vector<uint32_t> cnt(2 * (size_t)P.world + 1);
-  h->be.d2h(cnt.data(), P.cnt, cnt.size() * 4);
-  if (!rc) rc = h->be.sync();
+  uint64_t sums[4] = {0, 0, 0, 0};
+  if (!rc) {
+    h->be.reduce_launch(h->d_launch_dec, h->d_launch_ticks, h->d_launch_bytes, h->st.err, h->E, h->d_sums);
+    h->be.d2h_async(cnt.data(), P.cnt, cnt.size() * 4);
+    h->be.d2h_async(sums, h->d_sums, sizeof sums);
+    rc = h->be.sync();
+  }
   if (rc) return fail(std::string("sfl_part_local: ") + h->be.error());
+  h->last_kernel_ms = h->be.elapsed_ms();
+  h->last_dec = sums[0];
+  h->last_ticks = sums[1];
+  h->last_bytes = sums[2];
+  h->last_err = (uint32_t)sums[3];
+  h->total_dec += sums[0];
   uint64_t n = 0;
   for (int g = 0; g < P.world; ++g) n += cnt[g];
   if (n_req) *n_req = n;
-  return check_errors(h);
+  return scan_errors(h);
 }
 
 template <class B>
@@ -745,12 +762,11 @@ int part_update(Handle<B>* h, const void* upd_in) {
   if (!P.world) return fail("sfl_part_update: handle not partitioned");
   const PartUpd* in = (const PartUpd*)upd_in;
   uint32_t max_stage = 0;
-  for (int g = 0; g < P.world; ++g) {
-    PartUpd hd;
-    h->be.d2h(&hd, in + (size_t)g * (P.cap_upd + 1), sizeof hd);
-    if (h->be.sync()) return fail(h->be.error());
-    if (hd.genv > 0 && hd.state > max_stage) max_stage = hd.state;
-  }
+  std::vector<PartUpd> hd(P.world);
+  for (int g = 0; g < P.world; ++g) h->be.d2h_async(&hd[g], in + (size_t)g * (P.cap_upd + 1), sizeof(PartUpd));
+  if (h->be.sync()) return fail(h->be.error());
+  for (int g = 0; g < P.world; ++g)
+    if (hd[g].genv > 0 && hd[g].state > max_stage) max_stage = hd[g].state;
   for (uint32_t st = 0; st <= max_stage; ++st) h->be.part_update(h->map, P, in, (int)st);
   return h->be.sync() ? fail(std::string("sfl_part_update: ") + h->be.error()) : 0;
 }

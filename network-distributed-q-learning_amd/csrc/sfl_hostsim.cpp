@@ -25,6 +25,8 @@ struct HostBackend {
   void free(void* p) { ::free(p); }
   void h2d(void* d, const void* s, size_t n) { memcpy(d, s, n); }
   void d2h(void* d, const void* s, size_t n) { memcpy(d, s, n); }
+  void d2h_async(void* d, const void* s, size_t n) { memcpy(d, s, n); }
+  float elapsed_ms() { return 0.f; }
   void memset(void* p, int v, size_t n) { ::memset(p, v, n); }
   void fill_f64(double* p, double v, size_t n) {
     for (size_t i = 0; i < n; ++i) p[i] = v;
