@@ -41,8 +41,11 @@ __global__ void __launch_bounds__(SFL_WAVE_BLOCK) __attribute__((amdgpu_waves_pe
 }
 // maps with 65-128 trains (two train slots per lane): one env per 64-thread block (its LDS is
 // ~22 KB), register budget for the LDS-bound occupancy of 2 waves per SIMD
+#ifndef SFL_WAVE2_OCC
+#define SFL_WAVE2_OCC 2  // waves per SIMD k_wave2 is register-budgeted for
+#endif
 template <int PPL, int SPL, int TW, bool TRACE>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_wave2(const sfl::SflMap* __restrict__ m,
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SFL_WAVE2_OCC))) k_wave2(const sfl::SflMap* __restrict__ m,
                                                                                    const sfl::SflState* __restrict__ s,
                                                                                    const sfl::SflCtl* __restrict__ c) {
   sfl::wave::run<PPL, SPL, TW, TRACE>(*m, *s, *c);
@@ -56,7 +59,7 @@ k_wave_part(const sfl::SflMap* __restrict__ m, const sfl::SflState* __restrict__
   sfl::wave::run<PPL, SPL, TW, false, true>(*m, *s, *c, P);
 }
 template <int PPL, int SPL, int TW>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SFL_WAVE2_OCC)))
 k_wave2_part(const sfl::SflMap* __restrict__ m, const sfl::SflState* __restrict__ s, const sfl::SflCtl* __restrict__ c,
              const sfl::SflPart* __restrict__ P) {
   sfl::wave::run<PPL, SPL, TW, false, true>(*m, *s, *c, P);

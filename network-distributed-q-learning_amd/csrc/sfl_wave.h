@@ -46,11 +46,12 @@ __device__ unsigned long long g_prof[32];
 #endif
 
 constexpr uint32_t PF_NONE = 0xFFFFFFFFu;
-// batch-prefetch record per train (doubles): row 0-3, pending cell 4, slot word 5, the row's max 6,
-// then int32 words from PF_I: distance-map value at the train's cell (observation), at its
+// batch-prefetch record per train (doubles): the pending cell 0, the slot word 1, the staged row's
+// max 2, then int32 words from PF_I: distance-map value at the train's cell (observation), at its
 // projected cell if it stops (reward of STOP), if it moves with final rail action 0..3 (reward of
-// a route), and the row's argmax | first allowed argmax << 8 under the staged observation
-constexpr int PF_W = 12, PF_I = 14;
+// a route), and the row's argmax | first allowed argmax << 8 under the staged observation (the
+// row's columns themselves are not kept: a decision on a staged row needs only its max and argmaxes)
+constexpr int PF_W = 7, PF_I = 6;
 #ifndef SFL_WAVE_BLOCK
 #define SFL_WAVE_BLOCK 256  // threads per k_wave block (envs per block x 64)
 #endif
@@ -243,7 +244,7 @@ struct WEnv {
   uint32_t* lcnt;  // [64*SPL]
   // batch prefetch (see prefetch()): per queued train (lane), the staged Q row, the pending
   // update's Q cell value and the slot word in LDS, and the staged offsets in VGPRs
-  double* lpf;       // [64][PF_W]: row columns 0-3 | pending cell value | slot word (as bits) | int32 distances (PF_D0..)
+  double* lpf;       // [TW][PF_W]: pending cell value | slot word (as bits) | row max | int32 distances, argmaxes
   uint32_t pf_roff[TPL];  // offset of the staged row in the env's Q block (PF_NONE: none)
   uint32_t pf_qoff[TPL];  // offset of the staged pending cell (PF_NONE: none)
   bool pf_ok;        // uniform: this batch has been prefetched
@@ -1077,8 +1078,6 @@ struct WEnv {
       for (int c = 0; c < 4; ++c) rv[c] = ld(rp, (size_t)((uint32_t)c < w ? c : 0));
       qv = ld(qbase(), (size_t)(hp ? qoff : 0u));
     }
-#pragma unroll
-    for (int c = 0; c < 4; ++c) pfl[c] = rv[c];
     // the greedy choice on the staged row (distr_q.py:449-490, as in decide): valid whenever the
     // row is (a decision uses it only if its observation is the staged one)
     {
@@ -1109,11 +1108,11 @@ struct WEnv {
         arg = b2 ? a : arg;
         amx = b2 ? v : amx;
       }
-      pfl[6] = mx;
+      pfl[2] = mx;
       pfi[6] = (best & 0xFF) | ((arg & 0xFF) << 8);
     }
-    pfl[4] = qv;
-    pfl[5] = __longlong_as_double((long long)slw);
+    pfl[0] = qv;
+    pfl[1] = __longlong_as_double((long long)slw);
     pf_roff[ks] = (row_ok && !PART) ? roff : PF_NONE;
     pf_qoff[ks] = (hp && !PART) ? qoff : PF_NONE;
   }
@@ -1171,9 +1170,9 @@ struct WEnv {
     // the decision's LDS reads that do not depend on its observation, issued together: the staged
     // slot word (never stale: a decision writes only its own train's slots), row column, pending
     // cell value and distances, the epsilon-greedy stream and the switch's interaction count
-    const uint64_t slot_v = (uint64_t)__double_as_longlong(pfh[5]);
-    const double pf_qp = pfh[4];
-    const double pf_mx = pfh[6];
+    const uint64_t slot_v = (uint64_t)__double_as_longlong(pfh[1]);
+    const double pf_qp = pfh[0];
+    const double pf_mx = pfh[2];
     const vec_t<int32_t, 2> pfd01 = *(const vec_t<int32_t, 2>*)((const int32_t*)pfh + PF_I);
     const vec_t<int32_t, 2> pfd23 = *(const vec_t<int32_t, 2>*)((const int32_t*)pfh + PF_I + 2);
     const vec_t<int32_t, 2> pfd45 = *(const vec_t<int32_t, 2>*)((const int32_t*)pfh + PF_I + 4);
