@@ -142,14 +142,15 @@ def test_c5_small_batch(lib, kernel):
     assert b.q_dict(2) == model.q
 
 
-@pytest.mark.parametrize("cfg,E", [("c2", 256), ("c5", 64)])
+@pytest.mark.parametrize("cfg,E", [("c2", 256), ("c5", 64), ("golden:city6_s5", 128)])
 def test_partitioned_rounds_gpu_equal_fused(lib, cfg, E, kernel):
     """Graph-partitioned mode (BASELINE configs[4]) on the GPU, one rank: the owner-side Q rows,
     the request / reply / update round trips through device buffers, bit-equal to the fused kernel.
     kernel: the local step on k_wave (observe / apply passes, PART) or on the lane-per-env body."""
     import torch
     part = importlib.import_module("network-distributed-q-learning_amd.partition")
-    cm = comp.compile_scenario(mapgen.make_config(cfg))
+    sc = _golden.load(cfg[7:])["scenario_obj"] if cfg.startswith("golden:") else mapgen.make_config(cfg)
+    cm = comp.compile_scenario(sc)
     seeds = [2000 + i for i in range(E)]
     ref = runtime.Batch(cm, HP, seeds, lib=lib, ntab=1 << 14)
     ref.learn_begin()
@@ -172,13 +173,13 @@ def test_partitioned_rounds_gpu_equal_fused(lib, cfg, E, kernel):
     ref.close()
 
 
-@pytest.mark.parametrize("cfg", ["c2", "c5"])
-def test_two_rank_partition_wave_gpu(lib, cfg):
+@pytest.mark.parametrize("cfg,world", [("c2", 2), ("c5", 2), ("c5", 3)])
+def test_two_rank_partition_wave_gpu(lib, cfg, world):
     """Two ranks (processes) on GPU 0 over gloo: k_wave's PART local step with the row requests,
     replies and update records crossing ranks; each rank's owned Q rows, key set and env states
     bit-equal to the fused run of all envs (host build)."""
     from tests import test_partition
-    test_partition.two_rank_run(cfg, gpu=True)
+    test_partition.two_rank_run(cfg, gpu=True, world=world)
 
 
 @pytest.mark.parametrize("S,T,variant", [(64, 48, 3), (100, 48, 4), (120, 64, 4), (100, 100, 5), (200, 40, 5),

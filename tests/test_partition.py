@@ -130,17 +130,17 @@ def _worker(rank, world, port, cfg, q, gpu=False):
         raise
 
 
-def two_rank_run(cfg, gpu=False):
+def two_rank_run(cfg, gpu=False, world=2):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, cfg, q, gpu)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, cfg, q, gpu)) for r in range(world)]
     for p in procs:
         p.start()
-    res = sorted(q.get(timeout=600) for _ in range(2))
+    res = sorted(q.get(timeout=600) for _ in range(world))
     for p in procs:
         p.join(timeout=120)
-    assert res == [(0, "ok"), (1, "ok")], res
+    assert res == [(r, "ok") for r in range(world)], res
     for p in procs:
         assert p.exitcode == 0
 
