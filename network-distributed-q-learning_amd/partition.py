@@ -110,6 +110,7 @@ class PartitionedBatch:
             self.rep_send, self.rep_recv = z(nrep), z(nrep)
             self.upd_send, self.upd_recv = z(nupd), z(nupd)
         self.on_gpu = dev.type == "cuda"
+        self.rec = (rq.value, rp.value, up.value)
         self.rounds = 0
 
     def close(self):
@@ -138,6 +139,54 @@ class PartitionedBatch:
         if self.on_gpu:
             self.torch.cuda.current_stream().synchronize()
 
+    # ---- size-aware exchange (N > 1 ranks on NCCL/RCCL, or gloo with host buffers) ------------------
+    # Each destination segment's filled prefix (header record + its records) travels as one
+    # point-to-point message into the same place of the receiver's segment: the owner kernels
+    # read a segment only up to its header count, so nothing beyond the prefix is needed.
+    def _sized(self) -> bool:
+        return self.dist is not None and self.world > 1 and not (self.on_gpu and self.dist.get_backend() == "gloo")
+
+    def _header_counts(self, buf, cap, rec):
+        seg = buf.view(self.world, (cap + 1) * rec)
+        return seg[:, :4].contiguous().view(self.torch.int32).reshape(self.world).to(self.torch.int64)
+
+    def _p2p(self, recv, send, cap, rec, n_send, n_recv):
+        torch, dist = self.torch, self.dist
+        rs, ss = recv.view(self.world, (cap + 1) * rec), send.view(self.world, (cap + 1) * rec)
+        ops = []
+        for p in range(self.world):
+            k_s, k_r = (int(n_send[p]) + 1) * rec, (int(n_recv[p]) + 1) * rec
+            if p == self.rank:
+                rs[p, :k_r].copy_(ss[p, :k_s])
+                continue
+            ops.append(dist.P2POp(dist.isend, ss[p, :k_s], p))
+            ops.append(dist.P2POp(dist.irecv, rs[p, :k_r], p))
+        if ops:
+            for r in dist.batch_isend_irecv(ops):
+                r.wait()
+        if self.on_gpu:
+            torch.cuda.current_stream().synchronize()
+
+    def _exchange_sized(self):
+        """Updates and requests: counts first (one small all-to-all), then the filled prefixes."""
+        torch = self.torch
+        rq, _, up = self.rec
+        n_req = self._header_counts(self.req_send, self.cap_req, rq)
+        n_upd = self._header_counts(self.upd_send, self.cap_upd, up)
+        cs = torch.stack([n_req, n_upd], dim=1).contiguous()  # row d: what this rank sends to rank d
+        cr = torch.empty_like(cs)
+        self.dist.all_to_all_single(cr, cs)                    # row s: what rank s sends to this rank
+        cs, cr = cs.cpu().tolist(), cr.cpu().tolist()
+        self._n_req_sent = [c[0] for c in cs]
+        self._n_req_recv = [c[0] for c in cr]
+        self._p2p(self.upd_recv, self.upd_send, self.cap_upd, up, [c[1] for c in cs], [c[1] for c in cr])
+        self._p2p(self.req_recv, self.req_send, self.cap_req, rq, self._n_req_sent, self._n_req_recv)
+
+    def _exchange_replies_sized(self):
+        """A reply segment to rank s holds one reply per request received from s."""
+        rp = self.rec[1]
+        self._p2p(self.rep_recv, self.rep_send, self.cap_req, rp, self._n_req_recv, self._n_req_sent)
+
     def step(self, decisions_per_env: int) -> int:
         """Advance every local env by ``decisions_per_env`` learning decisions (the sfl_step contract);
         returns the number of rounds.  Collective over the ranks."""
@@ -145,16 +194,23 @@ class PartitionedBatch:
         h = self.batch.h
         ptr = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
         self.lib.check(d.sfl_part_begin(h), "sfl_part_begin")
+        sized = self._sized()
         rounds = 0
         for _ in range(int(decisions_per_env) + 1):
             n = C.c_uint64(0)
             self.lib.check(d.sfl_part_local(h, int(decisions_per_env), ptr(self.rep_recv), ptr(self.req_send),
                                             ptr(self.upd_send), C.byref(n)), "sfl_part_local")
-            self._exchange(self.upd_recv, self.upd_send)
-            self._exchange(self.req_recv, self.req_send)
+            if sized:
+                self._exchange_sized()
+            else:
+                self._exchange(self.upd_recv, self.upd_send)
+                self._exchange(self.req_recv, self.req_send)
             self.lib.check(d.sfl_part_update(h, ptr(self.upd_recv)), "sfl_part_update")
             self.lib.check(d.sfl_part_answer(h, ptr(self.req_recv), ptr(self.rep_send)), "sfl_part_answer")
-            self._exchange(self.rep_recv, self.rep_send)
+            if sized:
+                self._exchange_replies_sized()
+            else:
+                self._exchange(self.rep_recv, self.rep_send)
             rounds += 1
         if n.value != 0:
             raise _lib.SflError(f"rank {self.rank}: {n.value} requests still open after the last round")

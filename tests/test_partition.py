@@ -116,6 +116,8 @@ def _worker(rank, world, port, cfg, q, gpu=False):
                                    ntab=4096, **kw)
         if gpu:
             assert pb.batch.counters()["kernel_variant"] > 0
+        else:  # host buffers on gloo: the size-aware point-to-point exchange (the NCCL/RCCL path's code)
+            assert pb._sized()
         pb.learn_begin()
         pb.apply_qinit()
         for n in (90, 60):
@@ -145,6 +147,6 @@ def two_rank_run(cfg, gpu=False, world=2):
         assert p.exitcode == 0
 
 
-@pytest.mark.parametrize("cfg", ["c2", "c5"])
-def test_two_rank_partition_matches_fused(cfg):
-    two_rank_run(cfg)
+@pytest.mark.parametrize("cfg,world", [("c2", 2), ("c5", 2), ("c5", 3)])
+def test_two_rank_partition_matches_fused(cfg, world):
+    two_rank_run(cfg, world=world)
