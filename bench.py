@@ -28,8 +28,54 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 METRIC = "agent-env-steps/sec (whole node), 64-switch map, 1/2/4/8 MI355X vs CPU"
 
 
-def cpu_baseline(sc, seconds: float):
-    """The CPU oracle (pure-Python restatement of the reference loop), one env, one core."""
+def host_cores():
+    """(affinity core count, cgroup CPU quota in cores or None) of this process."""
+    n = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except Exception:
+        pass
+    return n, quota
+
+
+def cpu_baseline(cm, seconds: float):
+    """BASELINE.md / SURVEY.md §8(d): the build's C++ CPU backend -- the same kernel body compiled for
+    the host (libsfl_hostsim.so, OpenMP, one env per thread at a time) -- on ALL host cores of this
+    box (os.sched_getaffinity), 8 envs per core, same map, seeds and hyper-parameters, learning mode.
+    The reference loop itself cannot run here (flatland-rl is absent), so this is a "port"."""
+    import ctypes
+    build = importlib.import_module(PKG + ".build")
+    _lib = importlib.import_module(PKG + "._lib")
+    runtime = importlib.import_module(PKG + ".runtime")
+    cores, quota = host_cores()
+    lib = _lib.Lib(build.build_hostsim())
+    lib.check_fresh()
+    lib.dll.sflh_set_threads.restype = ctypes.c_int
+    threads = lib.dll.sflh_set_threads(ctypes.c_int(cores))
+    E = 8 * threads
+    b = runtime.Batch(cm, HP, [450565 + i for i in range(E)], lib=lib)
+    b.learn_begin()
+    b.apply_qinit()
+    b.step(64)
+    n = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        n += b.step(64)[0]
+    dt = time.perf_counter() - t0
+    b.close()
+    q = f", cgroup CPU quota {quota:g} cores" if quota else ""
+    return dict(value=n / dt, unit="agent-env-steps/sec", cores=threads, kind="port",
+                sample=f"libsfl_hostsim.so (the kernel body built for the host, OpenMP, {threads} threads = every core "
+                       f"of os.sched_getaffinity{q}) over {E} envs of the c3 map (seeds 450565+i), {n} decisions in "
+                       f"{dt:.1f} s after one untimed 64-decision step")
+
+
+def cpu_oracle_baseline(sc, seconds: float):
+    """Second data point: the CPU oracle (pure-Python restatement of the reference loop, the
+    reference's own speed class), one env, one core."""
     from oracle import sfl_oracle as so
     env, model = so.build(sc, 450565, HP, trace=False)
     state = None
@@ -42,32 +88,6 @@ def cpu_baseline(sc, seconds: float):
     return dict(value=n / dt, unit="agent-env-steps/sec", cores=1, kind="port",
                 sample=f"oracle/sfl_oracle.py learn loop, 1 env of the c3 map, {n} decisions in {dt:.1f} s "
                        f"(from episode start, incl. the Q-table init)")
-
-
-def cpu_cxx_baseline(cm, seconds: float):
-    """The build's C++ CPU backend: the same kernel body compiled for the host
-    (libsfl_hostsim.so, one env per OpenMP thread at a time) on the host cores, same map and
-    hyper-parameters, learning mode.  Reported beside cpu_baseline; not the product path."""
-    build = importlib.import_module(PKG + ".build")
-    _lib = importlib.import_module(PKG + "._lib")
-    runtime = importlib.import_module(PKG + ".runtime")
-    threads = int(os.environ.get("OMP_NUM_THREADS") or 0) or len(os.sched_getaffinity(0))
-    threads = max(1, min(threads, len(os.sched_getaffinity(0)), 16))
-    lib = _lib.Lib(build.build_hostsim())
-    E = 4 * threads
-    b = runtime.Batch(cm, HP, [450565 + i for i in range(E)], lib=lib)
-    b.learn_begin()
-    b.apply_qinit()
-    b.step(64)
-    n = 0
-    t0 = time.perf_counter()
-    while time.perf_counter() - t0 < seconds:
-        n += b.step(64)[0]
-    dt = time.perf_counter() - t0
-    b.close()
-    return dict(value=n / dt, unit="agent-env-steps/sec", cores=threads, kind="port",
-                sample=f"libsfl_hostsim.so (the kernel body built for the host, OpenMP over {E} envs of the c3 map), "
-                       f"{n} decisions in {dt:.1f} s after one untimed 64-decision step")
 
 
 def dist_setup(par, local: int):
@@ -121,6 +141,7 @@ def main():
     mapgen = importlib.import_module(PKG + ".mapgen")
     comp = importlib.import_module(PKG + ".compiler")
     runtime = importlib.import_module(PKG + ".runtime")
+    importlib.import_module(PKG + ".build").build_hip()  # (re)build if the library is not from these sources
     sc = mapgen.make_config(args.config)
     cm = comp.compile_scenario(sc)
     E = args.envs
@@ -175,8 +196,8 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic 64-switch/32-train Flatland-format map (mapgen c3, seed 450565), random-init "
-                    "(default_q + optimistic init) Q-tables",
+            "data": f"synthetic {cm.S}-switch/{cm.T}-train Flatland-format map (mapgen {args.config}, seed 450565), "
+                    "Q-tables at default_q + the optimistic init",
             "config": {"workload": workload,
                        "envs_per_gpu": E, "decisions_per_env_per_step": args.decisions,
                        "parallelism": f"env-batch dp{world}"},
@@ -187,8 +208,8 @@ def main():
                          "ticks_per_decision": ticks_l / max(1, dec_l)},
         }
         if world == 1 and not args.no_cpu:
-            res["cpu_baseline"] = cpu_baseline(sc, args.cpu_seconds)
-            res["cpu_cxx_baseline"] = cpu_cxx_baseline(cm, args.cpu_seconds)
+            res["cpu_baseline"] = cpu_baseline(cm, args.cpu_seconds)
+            res["cpu_oracle_baseline"] = cpu_oracle_baseline(sc, args.cpu_seconds / 2)
         print(json.dumps(res), flush=True)
     b.close()
     if dist is not None:
@@ -211,6 +232,7 @@ def bench_partition(args):
     E = args.envs if args.envs != 65536 else 16384
     cm = comp.compile_scenario(mapgen.make_config(cfg))
     seeds = par.shard_seeds(450565, E, rank)
+    importlib.import_module(PKG + ".build").build_hip()
     pb = part.PartitionedBatch(cm, HP, seeds, rank * E, world * E, rank=rank, world=world, dist=dist, device=dev,
                                buffer_device="cuda")
     pb.learn_begin()

@@ -16,12 +16,12 @@ ASyncSwitchEnv = importlib.import_module(PKG + ".env").ASyncSwitchEnv
 DistrQLearning = importlib.import_module(PKG + ".distr_q").DistrQLearning
 from main import build_scenario  # noqa: E402
 
-if __name__ == "__main__":
-    ap = argparse.ArgumentParser()
-    ap.add_argument("exp_dirs", nargs="+")
-    ap.add_argument("--model", default="distr_q_model.pkl")
-    args = ap.parse_args()
-    for exp_dir in args.exp_dirs:
+
+def evaluate(exp_dirs, model_file="distr_q_model.pkl", lib=None):
+    """eval.py:34-99: greedy test() runs of each experiment's saved Q-table.  ``lib``: the library
+    handle (default: the HIP product library; tests pass the host build)."""
+    results = {}
+    for exp_dir in exp_dirs:
         print(f"Evaluating {exp_dir}")
         config = configparser.ConfigParser()
         config.read(os.path.join(exp_dir, "config.ini"))
@@ -30,12 +30,23 @@ if __name__ == "__main__":
         model = DistrQLearning(env=env, gamma=float(m["gamma"]), epsilon=float(m["epsilon"]),
                                epsilon_decay_rate=float(m["epsilon_decay_rate"]), lr=float(m["lr"]),
                                lr_decay_rate=float(m["lr_decay_rate"]), default_q=float(m["default_q"]),
-                               seed=int(config["MISC"]["random_seed"]))
-        model.load(os.path.join(exp_dir, args.model))
+                               seed=int(config["MISC"]["random_seed"]), lib=lib)
+        model.load(os.path.join(exp_dir, model_file))
         num_evals = 10 if float(config["ENV"].get("malfunction_rate", 0)) > 0 else 1
+        runs = []
         for i in range(num_evals):
             print(f"Eval {i + 1}")
             out_dir = os.path.join(exp_dir, f"eval_{i}")
             os.makedirs(out_dir, exist_ok=True)
-            model.test(out_dir=out_dir, plot=False)
+            runs.append(model.test(out_dir=out_dir, plot=False))
             print("")
+        results[exp_dir] = runs
+    return results
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("exp_dirs", nargs="+")
+    ap.add_argument("--model", default="distr_q_model.pkl")
+    args = ap.parse_args()
+    evaluate(args.exp_dirs, args.model)

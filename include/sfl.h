@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define SFL_ABI_VERSION 3
+#define SFL_ABI_VERSION 4
 
 typedef struct sfl_handle sfl_handle;
 
@@ -119,6 +119,9 @@ typedef struct {
 } sfl_counters;
 
 int sfl_abi_version(void);
+/* SHA-1 of the sources the library was built from (build.py kernel_source_sha1); the Python
+ * loader refuses a library whose id differs from the sources in its tree (a stale build) */
+const char* sfl_build_id(void);
 const char* sfl_last_error(void);
 int sfl_device_count(int* n);
 

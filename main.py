@@ -5,6 +5,10 @@ Sections/keys as in the reference (main.py:21-60; writer hyperparam_tuning.py:49
   [ENV]   width, height, max_num_cities, max_rails_between_cities, max_rail_pairs_in_city,
           number_of_agents, malfunction_rate, min_duration, max_duration   (+ optional scenario:
           a mapgen config name or a scenario JSON path, used instead of the size keys)
+
+The size keys give mapgen's stand-in layout (mapgen.from_flatland_params), not Flatland's
+sparse_rail_generator output, which is absent: max_num_cities is honoured as a cap inside
+width x height, max_rails_between_cities / max_rail_pairs_in_city have no counterpart (warned).
   [MODEL] gamma, epsilon, epsilon_decay_rate, lr, lr_decay_rate, default_q, num_episodes
 """
 import argparse
@@ -29,11 +33,13 @@ def build_scenario(config):
         s = env["scenario"]
         sc = mapgen.make_config(s, seed=seed, malfunction=mf) if s in mapgen.CONFIGS else mapgen.Scenario.load(s)
         return sc
+    opt = {k: int(env[k]) for k in ("max_rails_between_cities", "max_rail_pairs_in_city") if k in env}
     return mapgen.from_flatland_params(int(env["width"]), int(env["height"]), int(env["max_num_cities"]),
-                                       int(env["number_of_agents"]), seed, malfunction=mf)
+                                       int(env["number_of_agents"]), seed, malfunction=mf, **opt)
 
 
-def launch_experiment(config_path):
+def launch_experiment(config_path, lib=None):
+    """``lib``: the library handle to run on (default: the HIP product library; tests pass the host build)."""
     start_time = time.time()
     config = configparser.ConfigParser()
     config.read(config_path)
@@ -48,7 +54,7 @@ def launch_experiment(config_path):
     model = DistrQLearning(env=env, gamma=float(m["gamma"]), epsilon=float(m["epsilon"]),
                            epsilon_decay_rate=float(m["epsilon_decay_rate"]), lr=float(m["lr"]),
                            lr_decay_rate=float(m["lr_decay_rate"]), default_q=float(m["default_q"]),
-                           seed=int(config["MISC"]["random_seed"]))
+                           seed=int(config["MISC"]["random_seed"]), lib=lib)
     n_ep = int(m["num_episodes"])
     model.learn(num_episodes=n_ep, out_dir=out_dir, checkpoint_freq=checkpoint_freq, exploit_freq=exploit_freq)
     model.save(os.path.join(out_dir, "distr_q_model.pkl"))

@@ -12,7 +12,7 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 PRODUCT_LIB = os.path.join(HERE, "libsfl.so")
-ABI_VERSION = 3  # include/sfl.h SFL_ABI_VERSION
+ABI_VERSION = 4  # include/sfl.h SFL_ABI_VERSION
 
 P = C.POINTER
 
@@ -60,6 +60,7 @@ class Counters(C.Structure):
 
 EXPORTS = {
     "sfl_abi_version": (C.c_int, []),
+    "sfl_build_id": (C.c_char_p, []),
     "sfl_last_error": (C.c_char_p, []),
     "sfl_device_count": (C.c_int, [P(C.c_int)]),
     "sfl_create": (C.c_int, [P(MapDesc), P(HParams), C.c_uint32, P(C.c_uint64), C.c_int, P(C.c_void_p)]),
@@ -103,6 +104,15 @@ class Lib:
             fn.argtypes = args
         if self.dll.sfl_abi_version() != ABI_VERSION:
             raise SflError("ABI version mismatch")
+        self.build_id = self.dll.sfl_build_id().decode()
+
+    def check_fresh(self):
+        """Refuse a library built from other sources than the ones in this tree (a stale build)."""
+        from . import build
+        want = build.kernel_source_sha1()
+        if self.build_id != want:
+            raise SflError(f"{self.path} is stale: built from sources {self.build_id[:12]}, the tree has {want[:12]} "
+                           f"(rebuild: python -c 'import __graft_entry__ as g; g.build()')")
 
     def check(self, rc: int, what: str):
         if rc != 0:
@@ -127,6 +137,7 @@ def load_product() -> Lib:
 
         # SFL_LIB: an alternative in-tree build of the same HIP sources (tuning sweeps)
         lib = Lib(os.environ.get("SFL_LIB", PRODUCT_LIB))
+        lib.check_fresh()
         if lib.device_count() < 1:
             raise SflError("libsfl.so loaded but no HIP device is visible: the SwitchFL hot path runs on MI355X only")
         _product = lib

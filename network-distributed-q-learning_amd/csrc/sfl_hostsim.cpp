@@ -3,6 +3,7 @@
 // algorithm against the CPU oracle in a container without a GPU.  Never loaded
 // by the product package (network-distributed-q-learning_amd/_lib.py only
 // loads libsfl.so and requires a HIP device).
+#include <omp.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -121,6 +122,11 @@ int sflh_rng_selftest(uint32_t seedseq_value, uint32_t n, uint64_t* out64, uint3
   sfl::pcg_from_seedseq(seedseq_value, g);
   for (uint32_t i = 0; i < n; ++i) outb[i] = sfl::pcg_bounded(g, bound);
   return 0;
+}
+// OpenMP threads of the host build (bench.py's CPU baseline runs it on every host core)
+int sflh_set_threads(int n) {
+  if (n > 0) omp_set_num_threads(n);
+  return omp_get_max_threads();
 }
 int sflh_mf_draw(uint64_t seed, uint64_t tick, uint64_t handle, uint64_t* z) {
   *z = sfl::mf_draw(seed, tick, handle);

@@ -1545,15 +1545,24 @@ struct WEnv {
       }
     }
     // every global write of the step from one lane-0 region
+    // (SFL_AB_*: timing-only tuning builds that drop one class of store, results invalid)
     if (lane == 0) {
       if (hp) {
+#ifndef SFL_AB_NO_QST
         st(qbase(), (size_t)d.qoff_pend, nv);
+#endif
+#ifndef SFL_AB_NO_TOUCH
         touch_row(d.row_pend);
+#endif
       }
+#ifndef SFL_AB_NO_TOUCH
       if (d.touch_cur || (hp && d.sw != ps)) touch_row(d.row_cur);
+#endif
+#ifndef SFL_AB_NO_SLOT
       st(slotb, slot_ix(d.sw, d.h), slot_make(PEND_NONE, slot_rew(d.slotword, epoch), epoch));
       st(slotb, slot_ix(d.next_sw, d.h),
          slot_make(pend_make((uint32_t)d.sw, (uint32_t)d.slot, d.state, (uint32_t)d.j), d.r_new, epoch));
+#endif
     }
     if (hp) pf_written(d.qoff_pend);
     // destination bonus for newly arrived trains (distr_q.py:344-356); lanes take switches.

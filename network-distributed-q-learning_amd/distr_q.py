@@ -74,17 +74,21 @@ class DistrQLearning:
         if f == 1 and num_episodes > 0:
             pre = b.test(1)
             b.lib.check(b.lib.dll.sfl_mark_exploit_done(b.h), "sfl_mark_exploit_done")
-        b.apply_qinit()
+        # checkpoints are written at the start of episode t with (t+1) % checkpoint_freq == 0, after
+        # that episode's exploit round (distr_q.py:278-294): when both fall on t, the greedy round
+        # runs here (its max_action key-set inserts belong in the checkpoint) and the kernel skips it.
+        # __init_q_table runs after episode 0's reset (distr_q.py:296-300), i.e. after checkpoint_1.
+        stops = [t for t in range(num_episodes) if checkpoint_freq and (t + 1) % checkpoint_freq == 0]
+        qinit_pending = True
+        if not stops or stops[0] != 0:
+            b.apply_qinit()
+            qinit_pending = False
         cum = np.zeros((num_episodes, E))
         arrived = np.zeros((num_episodes, E), np.int32)
         delays = np.zeros((num_episodes, T, E))
         mfs = np.zeros((num_episodes, E), np.int32)
         cum_x = np.zeros((num_episodes, E))
         arr_x = np.zeros((num_episodes, E), np.int32)
-        # checkpoints are written at the start of episode t with (t+1) % checkpoint_freq == 0, after
-        # that episode's exploit round (distr_q.py:278-294): when both fall on t, the greedy round
-        # runs here (its max_action key-set inserts belong in the checkpoint) and the kernel skips it
-        stops = [t for t in range(num_episodes) if checkpoint_freq and (t + 1) % checkpoint_freq == 0]
         pre_x = {}
         done = 0
         for stop in stops + [num_episodes]:
@@ -111,6 +115,9 @@ class DistrQLearning:
                 # the reference resets trains_at_destination just before saving it (distr_q.py:285 vs 293)
                 self._save(out_dir, f"trains_at_dest_checkpoint_{t + 1}.npz", np.array([]))
                 self._save(out_dir, f"num_malfunctions_checkpoint_{t + 1}.npz", self._env_major(mfs[:t]))
+                if qinit_pending:
+                    b.apply_qinit()
+                    qinit_pending = False
         if pre is not None:
             cum_x[0] = pre["cum_reward"][0]
             arr_x[0] = pre["arrived"][0]

@@ -441,14 +441,15 @@ def _straight(r0: int, c0: int, r1: int, c1: int, pairs: Dict[Tuple[int, int], S
 
 
 def city_network(n_lines: int, spacing: int, margin: int, cities: List[Tuple[int, int, int]],
-                 rng: np.random.Generator, slip_weights=(0.2, 0.3, 0.5)):
+                 rng: np.random.Generator, slip_weights=(0.2, 0.3, 0.5), size: Optional[int] = None):
     """A square backbone of ``n_lines`` x ``n_lines`` rail lines (the inter-city connections) with
     cities on horizontal backbone segments, the way Flatland's sparse_rail_generator lays out a
     city: ``P`` parallel tracks (the backbone line plus P-1 sidings two rows apart) between two
     throats, each siding joining the main line through a T switch whose trunk faces out of the
     city.  ``cities``: (row line i, column line j, tracks P) -- the city sits between column lines
-    j and j+1 on row line i.  Returns (grid, junction cells, per-city track cells, throat cells)."""
-    side_len = 2 * margin + (n_lines - 1) * spacing + 1
+    j and j+1 on row line i.  ``size``: pad the grid to at least size x size (empty cells).  Returns
+    (grid, junction cells, per-city track cells, throat cells)."""
+    side_len = max(size or 0, 2 * margin + (n_lines - 1) * spacing + 1)
     pos = [margin + k * spacing for k in range(n_lines)]
     pairs: Dict[Tuple[int, int], Set[FrozenSet[int]]] = {}
     for i in range(n_lines):
@@ -491,7 +492,8 @@ def city_network(n_lines: int, spacing: int, margin: int, cities: List[Tuple[int
 
 def generate_cities(n_cities: int, n_trains: int, seed: int, *, n_lines: Optional[int] = None, spacing: int = 20,
                     margin: int = 7, tracks: Tuple[int, int] = (2, 3), malfunction: Tuple[float, int, int] = (0.0, 0, 0),
-                    name: str = "", slip_weights=(0.2, 0.3, 0.5), max_tries: int = 200) -> Scenario:
+                    name: str = "", slip_weights=(0.2, 0.3, 0.5), max_tries: int = 200,
+                    size: Optional[int] = None) -> Scenario:
     """Flatland-like scenario: ``n_cities`` cities of 2-3 parallel tracks with one station each on a
     square backbone of inter-city lines; every train starts on a city track and targets the station
     of another city; timetable as flatland_patch/timetable_generators.py (``timetable``)."""
@@ -506,7 +508,8 @@ def generate_cities(n_cities: int, n_trains: int, seed: int, *, n_lines: Optiona
     for _ in range(max_tries):
         pick = sorted(int(x) for x in rng.choice(len(slots), size=n_cities, replace=False))
         cities = [(slots[q][0], slots[q][1], int(rng.integers(tracks[0], tracks[1] + 1))) for q in pick]
-        grid, junctions, city_tracks, throats = city_network(n_lines, spacing, margin, cities, rng, slip_weights)
+        grid, junctions, city_tracks, throats = city_network(n_lines, spacing, margin, cities, rng, slip_weights,
+                                                             size=size)
         if not strongly_connected(grid):
             continue
         near_junction = lambda rc: any((rc[0] + dr, rc[1] + dc) in junctions for dr, dc in DELTA)  # noqa: E731
@@ -574,25 +577,45 @@ def make_config(name: str, seed: int = MAP_SEED, malfunction=(0.01, 5, 15)) -> S
     return generate(seed=seed, malfunction=malfunction, name=name, **kw)
 
 
-def from_flatland_params(width: int, height: int, max_num_cities: int, number_of_agents: int, seed: int,
-                         malfunction=(0.0, 0, 0), spacing: int = 5, margin: int = 3) -> Scenario:
-    """Scenario for the reference's [ENV] config keys (main.py:21-60).
+CITY_SPACING = 18  # backbone line spacing a 3-track city needs (city_network: 4 P + 6 cells)
+CITY_MARGIN = 7
 
-    Flatland's sparse_rail_generator is absent; with two or more cities the map is a
-    ``generate_cities`` layout (cities of parallel tracks on a square backbone) at least
-    ``width`` x ``height``; with one city, a line grid of that size with one station."""
+
+def from_flatland_params(width: int, height: int, max_num_cities: int, number_of_agents: int, seed: int,
+                         malfunction=(0.0, 0, 0), spacing: int = 5, margin: int = 3,
+                         max_rails_between_cities: Optional[int] = None,
+                         max_rail_pairs_in_city: Optional[int] = None) -> Scenario:
+    """Scenario for the reference's [ENV] config keys (main.py:21-60) on a width x height grid.
+
+    Flatland's sparse_rail_generator is absent, so this is a stand-in layout, not its output (parity
+    of the generated map is unpinned).  With two or more cities: a ``generate_cities`` layout (cities
+    of parallel tracks on a square backbone of >= 3 x 3 lines) inside width x height;
+    ``max_num_cities`` is a cap, as in Flatland, which places as many cities as fit -- here the
+    largest backbone that fits the grid decides.  With one city, or a grid too small for a backbone
+    (< 51 cells), a line grid of that size with one station per city.
+    ``max_rails_between_cities`` / ``max_rail_pairs_in_city`` have no counterpart in the stand-in
+    layout (a warning says so when they are given)."""
+    import warnings
     size = max(int(width), int(height))
     n_cities, n_agents = int(max_num_cities), int(number_of_agents)
-    if n_cities >= 2:
-        n_lines = 2
-        while n_lines * (n_lines - 1) < n_cities:
+    if max_rails_between_cities is not None or max_rail_pairs_in_city is not None:
+        warnings.warn("max_rails_between_cities / max_rail_pairs_in_city are ignored: the map is mapgen's stand-in "
+                      "layout, not Flatland's sparse_rail_generator (absent)", stacklevel=2)
+    n_fit = (size - 2 * CITY_MARGIN - 1) // CITY_SPACING + 1  # backbone lines that fit the grid
+    if n_cities >= 2 and n_fit >= 3:  # (a two-line backbone is a loop a train cannot turn around on)
+        n_lines = 3
+        while n_lines * (n_lines - 1) < n_cities and n_lines < n_fit:
             n_lines += 1
-        c_margin = 7
-        c_spacing = max(18, -(-(size - 2 * c_margin - 1) // (n_lines - 1)))
+        cap = n_lines * (n_lines - 1)
+        if n_cities > cap:
+            warnings.warn(f"max_num_cities={n_cities}: only {cap} cities fit a {size}x{size} grid", stacklevel=2)
+            n_cities = cap
+        c_spacing = (size - 2 * CITY_MARGIN - 1) // (n_lines - 1)
         return generate_cities(n_cities, n_agents, seed=int(seed), n_lines=n_lines, spacing=c_spacing,
-                               margin=c_margin, malfunction=malfunction, name=f"flatland_{width}x{height}")
+                               margin=CITY_MARGIN, malfunction=malfunction, name=f"flatland_{width}x{height}",
+                               size=size)
     n_lines = max(3, (size - 2 * margin - 1) // spacing + 1)
     n_sw = n_lines * n_lines - 4
-    return generate(n_switches=n_sw, n_trains=n_agents, n_stations=1, seed=int(seed), nx_lines=n_lines,
-                    ny_lines=n_lines, spacing=spacing, margin=margin, size=size, malfunction=malfunction,
-                    name=f"flatland_{width}x{height}")
+    return generate(n_switches=n_sw, n_trains=n_agents, n_stations=max(1, min(n_cities, n_agents)), seed=int(seed),
+                    nx_lines=n_lines, ny_lines=n_lines, spacing=spacing, margin=margin, size=size,
+                    malfunction=malfunction, name=f"flatland_{width}x{height}")

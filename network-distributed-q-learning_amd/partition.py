@@ -87,7 +87,12 @@ class PartitionedBatch:
         self.E = self.batch.E
         self.env_base, self.envs_total = int(env_base), int(envs_total)
         self.owner = np.ascontiguousarray(owner if owner is not None else partition_switches(cm, world), np.int32)
-        self.cap_req = self.E
+        # a receiver's request segment from rank s must hold one request per env of s: size the
+        # segments by the largest rank's env count, and check the job's env ranges add up
+        e_max, e_sum = self._job_env_counts(buffer_device)
+        if e_sum != self.envs_total:
+            raise ValueError(f"envs_total={self.envs_total} but the ranks hold {e_sum} envs")
+        self.cap_req = e_max
         self.cap_upd = max(64, upd_per_env * self.E)
         self.lib.check(self.lib.dll.sfl_part_config(self.batch.h, self.rank, self.world, _ptr(self.owner, C.c_int32),
                                                     self.env_base, self.envs_total, self.cap_req, self.cap_upd),
@@ -115,6 +120,28 @@ class PartitionedBatch:
 
     def close(self):
         self.batch.close()
+
+    def _job_env_counts(self, buffer_device):
+        """(max, sum) of the ranks' local env counts (one small collective when world > 1)."""
+        if self.dist is None or self.world == 1:
+            return self.E, self.E
+        torch = self.torch
+        dev = "cuda" if (buffer_device == "cuda" and self.dist.get_backend() != "gloo") else "cpu"
+        t = torch.tensor([self.E, -self.E], dtype=torch.int64, device=dev)
+        mx = t.clone()
+        self.dist.all_reduce(mx, op=self.dist.ReduceOp.MAX)
+        sm = torch.tensor([self.E], dtype=torch.int64, device=dev)
+        self.dist.all_reduce(sm)
+        return int(mx[0]), int(sm[0])
+
+    def _any_rank(self, flag: int) -> int:
+        """MAX of a per-rank flag over the job (every rank gets the same answer)."""
+        if self.dist is None or self.world == 1:
+            return flag
+        dev = "cuda" if (self.on_gpu and self.dist.get_backend() != "gloo") else "cpu"
+        t = self.torch.tensor([flag], dtype=self.torch.int64, device=dev)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return int(t[0])
 
     # ---- the reference's learn() set-up, on the partitioned tables ----------------------------
     def learn_begin(self):
@@ -154,8 +181,11 @@ class PartitionedBatch:
         torch, dist = self.torch, self.dist
         rs, ss = recv.view(self.world, (cap + 1) * rec), send.view(self.world, (cap + 1) * rec)
         ops = []
+        row = (cap + 1) * rec
         for p in range(self.world):
             k_s, k_r = (int(n_send[p]) + 1) * rec, (int(n_recv[p]) + 1) * rec
+            if k_s > row or k_r > row:
+                raise _lib.SflError(f"rank {self.rank}: segment to/from rank {p} exceeds its capacity ({cap} records)")
             if p == self.rank:
                 rs[p, :k_r].copy_(ss[p, :k_s])
                 continue
@@ -167,20 +197,30 @@ class PartitionedBatch:
         if self.on_gpu:
             torch.cuda.current_stream().synchronize()
 
-    def _exchange_sized(self):
-        """Updates and requests: counts first (one small all-to-all), then the filled prefixes."""
+    def _exchange_sized(self, err: int = 0):
+        """Updates and requests: counts first (one small all-to-all, which also carries this rank's
+        error flag to every rank), then the filled prefixes.  Returns the job-wide error flag; on an
+        error nothing else is exchanged (every rank stops at the same point)."""
         torch = self.torch
         rq, _, up = self.rec
-        n_req = self._header_counts(self.req_send, self.cap_req, rq)
-        n_upd = self._header_counts(self.upd_send, self.cap_upd, up)
-        cs = torch.stack([n_req, n_upd], dim=1).contiguous()  # row d: what this rank sends to rank d
+        if err:
+            n_req = torch.zeros(self.world, dtype=torch.int64, device=self.req_send.device)
+            n_upd = n_req
+        else:
+            n_req = self._header_counts(self.req_send, self.cap_req, rq)
+            n_upd = self._header_counts(self.upd_send, self.cap_upd, up)
+        fl = torch.full_like(n_req, int(err))
+        cs = torch.stack([n_req, n_upd, fl], dim=1).contiguous()  # row d: what this rank sends to rank d
         cr = torch.empty_like(cs)
         self.dist.all_to_all_single(cr, cs)                    # row s: what rank s sends to this rank
         cs, cr = cs.cpu().tolist(), cr.cpu().tolist()
+        if any(c[2] for c in cr):
+            return 1
         self._n_req_sent = [c[0] for c in cs]
         self._n_req_recv = [c[0] for c in cr]
         self._p2p(self.upd_recv, self.upd_send, self.cap_upd, up, [c[1] for c in cs], [c[1] for c in cr])
         self._p2p(self.req_recv, self.req_send, self.cap_req, rq, self._n_req_sent, self._n_req_recv)
+        return 0
 
     def _exchange_replies_sized(self):
         """A reply segment to rank s holds one reply per request received from s."""
@@ -198,13 +238,21 @@ class PartitionedBatch:
         rounds = 0
         for _ in range(int(decisions_per_env) + 1):
             n = C.c_uint64(0)
-            self.lib.check(d.sfl_part_local(h, int(decisions_per_env), ptr(self.rep_recv), ptr(self.req_send),
-                                            ptr(self.upd_send), C.byref(n)), "sfl_part_local")
+            # a failure on one rank (error flags of its envs, message overflow) must stop every rank,
+            # or the others would wait forever in the next exchange: the flag travels with the counts
+            rc = d.sfl_part_local(h, int(decisions_per_env), ptr(self.rep_recv), ptr(self.req_send),
+                                  ptr(self.upd_send), C.byref(n))
+            msg = self.lib.dll.sfl_last_error().decode(errors="replace") if rc else ""
             if sized:
-                self._exchange_sized()
+                failed = self._exchange_sized(err=1 if rc else 0)
             else:
-                self._exchange(self.upd_recv, self.upd_send)
-                self._exchange(self.req_recv, self.req_send)
+                failed = self._any_rank(1 if rc else 0)
+                if not failed:
+                    self._exchange(self.upd_recv, self.upd_send)
+                    self._exchange(self.req_recv, self.req_send)
+            if failed:
+                raise _lib.SflError(f"rank {self.rank}: sfl_part_local: " +
+                                    (msg or "stopped because another rank failed"))
             self.lib.check(d.sfl_part_update(h, ptr(self.upd_recv)), "sfl_part_update")
             self.lib.check(d.sfl_part_answer(h, ptr(self.req_recv), ptr(self.rep_send)), "sfl_part_answer")
             if sized:
@@ -212,8 +260,9 @@ class PartitionedBatch:
             else:
                 self._exchange(self.rep_recv, self.rep_send)
             rounds += 1
-        if n.value != 0:
-            raise _lib.SflError(f"rank {self.rank}: {n.value} requests still open after the last round")
+        if self._any_rank(1 if n.value != 0 else 0):
+            raise _lib.SflError(f"rank {self.rank}: requests still open after the last round "
+                                f"({n.value} on this rank)")
         self.rounds += rounds
         return rounds
 

@@ -12,4 +12,5 @@ def lib():
     if "lib" not in _cache:
         path = pkg_build.build_hostsim()
         _cache["lib"] = _lib.Lib(path)
+        _cache["lib"].check_fresh()
     return _cache["lib"]

@@ -16,12 +16,17 @@ def _load(d, f):
     return np.load(os.path.join(d, f + ".npz"))["x"]
 
 
+def _host():
+    return hostsim.lib()
+
+
 @pytest.mark.parametrize("name", ["c1_s7", "c2_mf"])
-def test_learn_outputs_match_reference_files(tmp_path, name):
+def test_learn_outputs_match_reference_files(tmp_path, name, lib=None):
+    lib = lib or _host()
     g = _golden.load(name)
     hp = g["hparams"]
     env = envmod.ASyncSwitchEnv(g["scenario_obj"], max_steps=hp.get("max_steps", 100_000))
-    model = dq.DistrQLearning(env, seed=g["seed"], lib=hostsim.lib(), **{k: hp[k] for k in
+    model = dq.DistrQLearning(env, seed=g["seed"], lib=lib, **{k: hp[k] for k in
                               ("gamma", "epsilon", "epsilon_decay_rate", "lr", "lr_decay_rate", "default_q")})
     model.learn(g["n_episodes"], str(tmp_path), checkpoint_freq=5, exploit_freq=g["exploit_freq"])
     ref = g["learn"]["outputs"]
@@ -42,17 +47,18 @@ def test_learn_outputs_match_reference_files(tmp_path, name):
     with open(tmp_path / "m.pkl", "rb") as f:
         assert pickle.load(f) == ref_q
     # load into a fresh learner, then the greedy test reproduces the reference's test()
-    model2 = dq.DistrQLearning(env, seed=g["seed"], lib=hostsim.lib(), **{k: hp[k] for k in
+    model2 = dq.DistrQLearning(env, seed=g["seed"], lib=lib, **{k: hp[k] for k in
                                ("gamma", "epsilon", "epsilon_decay_rate", "lr", "lr_decay_rate", "default_q")})
     model2.load(str(tmp_path / "m.pkl"))
     cr, arr, delays = model2.test(str(tmp_path), save_outputs=True)
     assert (cr, arr, delays) == (g["test"]["cum_reward"], g["test"]["arrived"], g["test"]["delays"])
 
 
-def test_batch_outputs_have_env_axis(tmp_path):
+def test_batch_outputs_have_env_axis(tmp_path, lib=None):
+    lib = lib or _host()
     g = _golden.load("c1_mf")
     env = envmod.ASyncSwitchEnv(g["scenario_obj"], max_steps=100_000, n_envs=3)
-    model = dq.DistrQLearning(env, seed=g["seed"], lib=hostsim.lib(), **{k: g["hparams"][k] for k in
+    model = dq.DistrQLearning(env, seed=g["seed"], lib=lib, **{k: g["hparams"][k] for k in
                               ("gamma", "epsilon", "epsilon_decay_rate", "lr", "lr_decay_rate", "default_q")})
     model.learn(4, str(tmp_path), checkpoint_freq=100)
     cr = _load(tmp_path, "cum_reward")
@@ -62,17 +68,18 @@ def test_batch_outputs_have_env_axis(tmp_path):
 
 
 @pytest.mark.parametrize("name", ["c2_s3", "city6_s5"])
-def test_checkpoint_after_coinciding_exploit_round(tmp_path, name):
+def test_checkpoint_after_coinciding_exploit_round(tmp_path, name, lib=None):
     """distr_q.py:278-294: when an exploit round and a checkpoint fall on the same episode, the
     exploit round (test(), whose max_action inserts keys) runs first and the checkpoint pickles the
     Q dict after it.  Checked against the oracle's snapshots at the same points."""
     from oracle import sfl_oracle as so
+    lib = lib or _host()
     g = _golden.load(name)
     hp = g["hparams"]
     f = g["exploit_freq"]
     n = 3 * f + 1
     env = envmod.ASyncSwitchEnv(g["scenario_obj"], max_steps=100_000)
-    model = dq.DistrQLearning(env, seed=g["seed"], lib=hostsim.lib(), **{k: hp[k] for k in
+    model = dq.DistrQLearning(env, seed=g["seed"], lib=lib, **{k: hp[k] for k in
                               ("gamma", "epsilon", "epsilon_decay_rate", "lr", "lr_decay_rate", "default_q")})
     model.learn(n, str(tmp_path), checkpoint_freq=f, exploit_freq=f)
     _, om = so.build(g["scenario_obj"], g["seed"], hp, trace=False)
@@ -85,3 +92,47 @@ def test_checkpoint_after_coinciding_exploit_round(tmp_path, name):
     assert _load(tmp_path, "cum_reward_exploit").tolist() == ref["cum_reward_exploit"]
     assert _load(tmp_path, "arrived_trains_exploit").tolist() == ref["arrived_trains_exploit"]
     assert model.q_table == om.q
+
+
+@pytest.mark.parametrize("exploit", [None, 1])
+def test_checkpoint_every_episode(tmp_path, exploit, lib=None):
+    """checkpoint_freq=1: checkpoint_1 is pickled before __init_q_table (distr_q.py:288-300), so it
+    holds no optimistic-init rows -- only what the t=0 exploit round's max_action inserted."""
+    from oracle import sfl_oracle as so
+    lib = lib or _host()
+    g = _golden.load("c1_s7")
+    hp = g["hparams"]
+    n = 4
+    env = envmod.ASyncSwitchEnv(g["scenario_obj"], max_steps=100_000)
+    model = dq.DistrQLearning(env, seed=g["seed"], lib=lib, **{k: hp[k] for k in
+                              ("gamma", "epsilon", "epsilon_decay_rate", "lr", "lr_decay_rate", "default_q")})
+    model.learn(n, str(tmp_path), checkpoint_freq=1, exploit_freq=exploit)
+    _, om = so.build(g["scenario_obj"], g["seed"], hp, trace=False)
+    ref = om.learn(n, exploit_freq=exploit, checkpoint_freq=1)
+    assert sorted(ref["checkpoints"]) == [1, 2, 3, 4]
+    if exploit is None:
+        assert ref["checkpoints"][1] == {}
+    for t1, q in ref["checkpoints"].items():
+        with open(tmp_path / f"checkpoint_{t1}.pkl", "rb") as fh:
+            assert pickle.load(fh) == q, t1
+    assert _load(tmp_path, "cum_reward").tolist() == ref["cum_reward"]
+    assert model.q_table == om.q
+
+
+def test_load_reference_pickle_format(tmp_path, lib=None):
+    """DistrQLearning.load on a pickle in the reference's own format: keys are tuple(observation) of
+    np.int64 (distr_q.py:56-57, 521-527), values lists of Python / numpy floats."""
+    lib = lib or _host()
+    g = _golden.load("c2_mf")
+    hp = g["hparams"]
+    ref_q = {tuple(np.int64(x) for x in k): [np.float64(v) if i % 2 else float(v) for i, v in enumerate(vals)]
+             for k, vals in g["learn"]["q_final"]}
+    with open(tmp_path / "ref.pkl", "wb") as f:
+        pickle.dump(ref_q, f)
+    env = envmod.ASyncSwitchEnv(g["scenario_obj"], max_steps=100_000)
+    model = dq.DistrQLearning(env, seed=g["seed"], lib=lib, **{k: hp[k] for k in
+                              ("gamma", "epsilon", "epsilon_decay_rate", "lr", "lr_decay_rate", "default_q")})
+    model.load(str(tmp_path / "ref.pkl"))
+    assert model.q_table == {tuple(int(x) for x in k): [float(v) for v in vals] for k, vals in ref_q.items()}
+    cr, arr, delays = model.test(str(tmp_path), save_outputs=False)
+    assert (cr, arr, delays) == (g["test"]["cum_reward"], g["test"]["arrived"], g["test"]["delays"])

@@ -1,0 +1,68 @@
+"""The reference's entry points on the host build: ``main.py -c config.ini`` (main.py:13-78) writes
+the reference's .npz / .pkl set, and ``eval.py`` (eval.py:34-99) reloads the saved Q-table and runs
+the greedy evaluations.  Outputs are compared with the golden vectors recorded from the reference."""
+import configparser
+import importlib
+import os
+import pickle
+
+import numpy as np
+import pytest
+
+from tests import _golden, hostsim
+
+main = importlib.import_module("main")
+evalmod = importlib.import_module("eval")
+
+
+def _load(d, f):
+    return np.load(os.path.join(d, f + ".npz"))["x"]
+
+
+def _write_ini(path, g, sc_path, exp_dir):
+    hp = g["hparams"]
+    sc = g["scenario_obj"]
+    cfg = configparser.ConfigParser()
+    cfg["MISC"] = dict(random_seed=g["seed"], out_dir=exp_dir, checkpoint_freq=1000, exploit_freq=g["exploit_freq"])
+    cfg["ENV"] = dict(scenario=sc_path, malfunction_rate=sc.malfunction_rate, min_duration=sc.malfunction_min,
+                      max_duration=sc.malfunction_max)
+    cfg["MODEL"] = dict(num_episodes=g["n_episodes"], **{k: hp[k] for k in
+                        ("gamma", "epsilon", "epsilon_decay_rate", "lr", "lr_decay_rate", "default_q")})
+    with open(path, "w") as f:
+        cfg.write(f)
+
+
+@pytest.mark.parametrize("name", ["c1_s7", "city6_s5"])
+def test_main_ini_then_eval(tmp_path, name):
+    g = _golden.load(name)
+    exp = tmp_path / "exp"
+    exp.mkdir()
+    sc_path = str(tmp_path / "scenario.json")
+    g["scenario_obj"].save(sc_path)
+    _write_ini(exp / "config.ini", g, sc_path, str(exp))
+    main.launch_experiment(str(exp / "config.ini"), lib=hostsim.lib())
+    ref = g["learn"]["outputs"]
+    for key, f in (("cum_reward", "cum_reward"), ("arrived_trains", "arrived_trains"), ("delays", "delays"),
+                   ("num_malfunctions", "num_malfunctions"), ("trains_at_dest", "trains_at_dest"),
+                   ("cum_reward_exploit", "cum_reward_exploit"), ("arrived_trains_exploit", "arrived_trains_exploit")):
+        assert _load(exp, f).tolist() == ref[key], key
+    with open(exp / "distr_q_model.pkl", "rb") as fh:
+        assert pickle.load(fh) == {tuple(k): v for k, v in g["learn"]["q_final"]}
+    res = evalmod.evaluate([str(exp)], lib=hostsim.lib())[str(exp)]
+    n_evals = 10 if g["scenario_obj"].malfunction_rate > 0 else 1
+    assert len(res) == n_evals
+    for i, (cr, arr, delays) in enumerate(res):
+        assert (cr, arr, delays) == (g["test"]["cum_reward"], g["test"]["arrived"], g["test"]["delays"]), i
+        assert float(_load(exp / f"eval_{i}", "cum_reward")) == g["test"]["cum_reward"]
+
+
+def test_main_ini_size_keys_honour_the_grid(tmp_path):
+    """[ENV] size keys of the reference's sweep (hyperparam_tuning.py:17-25): an 80 x 80 grid, the city
+    count capped to what fits, the Flatland-only keys warned about."""
+    cfg = configparser.ConfigParser()
+    cfg["MISC"] = dict(random_seed=64)
+    cfg["ENV"] = dict(width=80, height=80, max_num_cities=25, max_rails_between_cities=2, max_rail_pairs_in_city=2,
+                      number_of_agents=15, malfunction_rate=0.0, min_duration=0, max_duration=0)
+    with pytest.warns(UserWarning):
+        sc = main.build_scenario(cfg)
+    assert (sc.width, sc.height) == (80, 80) and len(sc.trains) == 15

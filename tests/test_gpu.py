@@ -208,3 +208,138 @@ def test_wave_kernel_shapes(lib, S, T, variant):
     assert bg.q_dict(5) == model.q
     bg.close()
     bh.close()
+
+
+# ---- the bench horizon and the reference's API on the product library ---------------------------
+
+def _spread(E, n=64, stride=1021):
+    """n env indices spread over the batch (different blocks, CUs and XCDs)."""
+    return sorted({(k * stride) % E for k in range(n)} | {0, E - 1})
+
+
+def _env_state(b, env):
+    import ctypes as C
+    cm = b.cm
+    el, ph = C.c_int32(), C.c_int32()
+    sem = np.zeros(4 * cm.S, np.uint64)
+    pos = np.zeros(cm.T, np.int32)
+    bits = np.zeros(cm.T, np.uint32)
+    P = C.POINTER
+    b.lib.check(b.lib.dll.sfl_get_env_state(b.h, env, C.byref(el), C.byref(ph), sem.ctypes.data_as(P(C.c_uint64)),
+                                            pos.ctypes.data_as(P(C.c_int32)), bits.ctypes.data_as(P(C.c_uint32))),
+                "sfl_get_env_state")
+    return el.value, ph.value, sem, pos, bits
+
+
+def test_c3_full_size_bench_horizon(lib):
+    """BASELINE configs[2] at the bench's size AND horizon: 65,536 envs, 2,560 decisions each in
+    bench-sized launches (every env crosses >= 2 episode ends: resets, arrival bonuses, truncation
+    and the (switch, train) slot epochs).  66 envs spread over the grid bit-equal to the host build
+    (Q-table, key set, semaphores, trains), 3 of them to the oracle."""
+    from tests import hostsim
+    sc = mapgen.make_config("c3")
+    cm = comp.compile_scenario(sc)
+    E = 65536
+    seeds = [450565 + i for i in range(E)]
+    chunks = (1024, 512, 1024)
+    b = runtime.Batch(cm, HP, seeds, lib=lib)
+    assert b.counters()["kernel_variant"] > 0
+    b.learn_begin()
+    b.apply_qinit()
+    for n in chunks:
+        got, ms = b.step(n)
+        assert got == n * E and ms > 0
+    assert b.counters()["decisions"] == sum(chunks) * E
+    pick = _spread(E)
+    bh = runtime.Batch(cm, HP, [seeds[e] for e in pick], lib=hostsim.lib())
+    bh.learn_begin()
+    bh.apply_qinit()
+    for n in chunks:
+        bh.step(n)
+    for i, e in enumerate(pick):
+        qg, tg = b.q_raw(e)
+        qh, th = bh.q_raw(i)
+        assert np.array_equal(qg, qh) and np.array_equal(tg, th), f"env {e}"
+        sg, sh = _env_state(b, e), _env_state(bh, i)
+        assert sg[0] == sh[0] and sg[1] == sh[1], f"env {e}"
+        for x, y in zip(sg[2:], sh[2:]):
+            assert np.array_equal(x, y), f"env {e}"
+    for e in (0, pick[len(pick) // 2], E - 1):
+        env, model = so.build(sc, seeds[e], HP, trace=False)
+        st = so.run_decisions(model, sum(chunks))
+        assert st["t"] >= 2, "the horizon must cross episode ends"
+        assert b.q_dict(e) == model.q, f"env {e}"
+    bh.close()
+    b.close()
+
+
+def test_c2_stated_batch_4096(lib):
+    """BASELINE configs[1] at its stated size: 16-switch / 8-train map, 4,096 envs, every env
+    bit-equal to the host build after 1,200 decisions (many episodes)."""
+    from tests import hostsim
+    sc = mapgen.make_config("c2")
+    cm = comp.compile_scenario(sc)
+    E = 4096
+    seeds = [450565 + i for i in range(E)]
+    bg = runtime.Batch(cm, HP, seeds, lib=lib)
+    assert bg.counters()["kernel_variant"] > 0
+    bh = runtime.Batch(cm, HP, seeds, lib=hostsim.lib())
+    for b in (bg, bh):
+        b.learn_begin()
+        b.apply_qinit()
+        for n in (200, 1000):
+            assert b.step(n)[0] == n * E
+    for e in range(E):
+        qg, tg = bg.q_raw(e)
+        qh, th = bh.q_raw(e)
+        assert np.array_equal(qg, qh) and np.array_equal(tg, th), f"env {e}"
+    env, model = so.build(sc, seeds[4095], HP, trace=False)
+    so.run_decisions(model, 1200)
+    assert bg.q_dict(4095) == model.q
+    bg.close()
+    bh.close()
+
+
+def test_device_pow_beyond_tables(lib, kernel):
+    """ntab = 16: epsilon and lr beyond the host tables come from the device's pow (pow_ool), with
+    decaying epsilon AND lr, checked against the oracle's Python ``**`` (distr_q.py:59-79)."""
+    hp = dict(gamma=0.95, epsilon=0.3, epsilon_decay_rate=0.99, lr=0.2, lr_decay_rate=0.999, default_q=-5.0)
+    sc = mapgen.make_config("c2")
+    cm = comp.compile_scenario(sc)
+    seeds = [77 + i for i in range(128)]
+    b = runtime.Batch(cm, hp, seeds, lib=lib, ntab=16)
+    _check_kernel(b, kernel)
+    b.learn_begin()
+    b.apply_qinit()
+    b.step(900)
+    for e in (0, 64, 127):
+        env, model = so.build(sc, seeds[e], hp, trace=False)
+        st = so.run_decisions(model, 900)
+        assert max(st["counts"].values()) > 16  # the pow path ran
+        assert b.q_dict(e) == model.q, f"env {e}"
+    b.close()
+
+
+@pytest.mark.parametrize("name", ["c1_s7", "c2_mf"])
+def test_distr_q_learn_outputs_gpu(lib, tmp_path, name):
+    """DistrQLearning.learn / save / load / test through libsfl.so: the reference's .npz set and
+    .pkl dict equal the golden vectors recorded from the reference."""
+    from tests import test_api_hostsim as api
+    api.test_learn_outputs_match_reference_files(tmp_path, name, lib=lib)
+
+
+@pytest.mark.parametrize("name", ["c2_s3", "city6_s5"])
+def test_distr_q_checkpoint_exploit_gpu(lib, tmp_path, name):
+    from tests import test_api_hostsim as api
+    api.test_checkpoint_after_coinciding_exploit_round(tmp_path, name, lib=lib)
+
+
+@pytest.mark.parametrize("exploit", [None, 1])
+def test_distr_q_checkpoint_every_episode_gpu(lib, tmp_path, exploit):
+    from tests import test_api_hostsim as api
+    api.test_checkpoint_every_episode(tmp_path, exploit, lib=lib)
+
+
+def test_distr_q_load_reference_pickle_gpu(lib, tmp_path):
+    from tests import test_api_hostsim as api
+    api.test_load_reference_pickle_format(tmp_path, lib=lib)

@@ -31,3 +31,23 @@ def test_step_matches_oracle(cfg, chunks):
         env, model = so.build(sc, seeds[e], HP, trace=False)
         so.run_decisions(model, total)
         assert b.q_dict(e) == model.q, f"env {e}"
+
+
+def test_pow_beyond_tables_host_build():
+    """ntab = 16 on the host build: epsilon and lr beyond the host tables come from pow, checked
+    against the oracle's Python ``**`` (distr_q.py:59-79); tests/test_gpu.py runs the device pow."""
+    from oracle import sfl_oracle as so2
+    hp = dict(gamma=0.95, epsilon=0.3, epsilon_decay_rate=0.99, lr=0.2, lr_decay_rate=0.999, default_q=-5.0)
+    sc = mapgen.make_config("c2")
+    cm = comp.compile_scenario(sc)
+    seeds = [77, 78]
+    b = runtime.Batch(cm, hp, seeds, lib=hostsim.lib(), ntab=16)
+    b.learn_begin()
+    b.apply_qinit()
+    b.step(900)
+    for e in range(2):
+        env, model = so2.build(sc, seeds[e], hp, trace=False)
+        st = so2.run_decisions(model, 900)
+        assert max(st["counts"].values()) > 16
+        assert b.q_dict(e) == model.q
+    b.close()
