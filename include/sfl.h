@@ -140,6 +140,9 @@ int sfl_step(sfl_handle* h, int64_t decisions_per_env, uint64_t* decisions_done,
 int sfl_get_q(sfl_handle* h, uint32_t env, double* q /* [q_per_env] */, uint32_t* touched /* [(rows+31)/32] */);
 int sfl_set_q(sfl_handle* h, uint32_t env, const double* q, const uint32_t* touched);
 int sfl_get_counters(sfl_handle* h, sfl_counters* out);
+/* why this handle runs the lane-per-env body (kernel_variant 0) instead of the one-env-per-wavefront
+ * kernel, e.g. "timetable horizon beyond 8191 ticks"; "" when it runs k_wave or k_run was requested */
+int sfl_get_kernel_note(sfl_handle* h, char* buf, int32_t cap);
 /* read back one env's state word arrays (debug / parity tests) */
 int sfl_get_env_state(sfl_handle* h, uint32_t env, int32_t* elapsed, int32_t* phase, uint64_t* sem /* [4S] */,
                       int32_t* tr_pos /* [T] */, uint32_t* tr_bits /* [T] */);

@@ -74,6 +74,7 @@ EXPORTS = {
     "sfl_get_q": (C.c_int, [C.c_void_p, C.c_uint32, P(C.c_double), P(C.c_uint32)]),
     "sfl_set_q": (C.c_int, [C.c_void_p, C.c_uint32, P(C.c_double), P(C.c_uint32)]),
     "sfl_get_counters": (C.c_int, [C.c_void_p, P(Counters)]),
+    "sfl_get_kernel_note": (C.c_int, [C.c_void_p, C.c_char_p, C.c_int32]),
     "sfl_get_env_state": (C.c_int, [C.c_void_p, C.c_uint32, P(C.c_int32), P(C.c_int32), P(C.c_uint64),
                                     P(C.c_int32), P(C.c_uint32)]),
     # graph-partitioned mode (partition.py)

@@ -23,6 +23,7 @@ numbering:
 """
 from __future__ import annotations
 
+import functools
 import itertools
 import math
 from dataclasses import dataclass, field
@@ -478,11 +479,19 @@ def _q_init_patch(cm: CompiledMap, grid, dist_k, tr_k) -> Dict[Tuple[int, int, i
     return patch
 
 
+@functools.lru_cache(maxsize=8)
+def _pow_table(x0: float, decay: float, n: int) -> np.ndarray:
+    # Python float ``**`` (the host libm's pow, as in the reference), not numpy's vectorised power
+    t = np.array([x0 * (decay ** k) for k in range(n)], dtype=np.float64)
+    t.setflags(write=False)
+    return t
+
+
 def eps_table(eps0: float, decay: float, n: int = NTAB) -> np.ndarray:
     """``initial_epsilon * decay ** t`` with Python float arithmetic (distr_q.py:68)."""
-    return np.array([eps0 * (decay ** t) for t in range(n)], dtype=np.float64)
+    return _pow_table(float(eps0), float(decay), int(n))
 
 
 def lr_table(lr0: float, decay: float, n: int = NTAB) -> np.ndarray:
     """``initial_lr * lr_decay ** t`` (distr_q.py:79)."""
-    return np.array([lr0 * (decay ** t) for t in range(n)], dtype=np.float64)
+    return _pow_table(float(lr0), float(decay), int(n))

@@ -36,6 +36,9 @@ enum : uint32_t {
   E_PLAN_OVF = 2,      // train plan longer than the packed ring
   E_PORT = 4,          // active train's next port not at the deciding switch (observer.py:294-301)
   E_BAD_ACTION = 8,    // action outside the switch's action space (switch_env.py:213-215)
+  // (16: E_MSG_OVF, sfl_part.h)
+  E_LR_TABLE = 32,     // device: a decayed lr beyond the host table; the device pow is not the host
+                       // libm's, so the run stops rather than lose bit-exactness (raise ntab)
 };
 
 constexpr int32_t DIST_INF = 0x3FFFFFFF;
@@ -477,7 +480,15 @@ struct Env {
     s.touched[(size_t)e * m.touched_words + (row >> 5)] |= 1u << (row & 31u);
   }
   SFL_FN double eps_of(uint32_t n) const { return n < (uint32_t)m.ntab ? m.eps_tab[n] : m.eps0 * pow(m.eps_decay, (double)n); }
-  SFL_FN double lr_of(uint32_t n) const { return n < (uint32_t)m.ntab ? m.lr_tab[n] : m.lr0 * pow(m.lr_decay, (double)n); }
+  // beyond the table: eps only decides `random() < eps` (an ulp of pow moves that by ~1e-17 in
+  // probability), but lr enters the Q values, so on the device a decaying lr past the table is an error
+  SFL_FN double lr_of(uint32_t n, uint32_t& e) const {
+    if (n < (uint32_t)m.ntab) return m.lr_tab[n];
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (m.lr_decay != 1.0) e |= E_LR_TABLE;
+#endif
+    return m.lr0 * pow(m.lr_decay, (double)n);
+  }
 
   // rng ------------------------------------------------------------------------
   SFL_FN Pcg64 rng_load() const {
@@ -1070,7 +1081,7 @@ SFL_FN void env_post(V& v, const Decision& d, Q& q) {
     const uint32_t pstate = (pend >> 14) & 0x3FFFu;
     const int pj = (int)((pend >> 28) & 3u);
     q.touch(ps, pslot, pstate);
-    const double lr = v.lr_of(s.counts[v.ix(ps)]);
+    const double lr = v.lr_of(s.counts[v.ix(ps)], v.err);
     const double r = (double)d.reward;
     if (d.sw != ps) {
       q.touch(d.sw, d.slot, d.state);
@@ -1102,7 +1113,7 @@ SFL_FN void env_post(V& v, const Decision& d, Q& q) {
         const uint32_t pstate = (pe >> 14) & 0x3FFFu;
         const int pj = (int)((pe >> 28) & 3u);
         q.touch(ps, pslot, pstate);
-        const double lr = v.lr_of(s.counts[v.ix(ps)]);
+        const double lr = v.lr_of(s.counts[v.ix(ps)], v.err);
         q.update(ps, pslot, pstate, pj, lr, 1000.0 + m.gamma * 0.0, stage);
         sl = slot_make(PEND_NONE, slot_rew(sl, v.epoch), v.epoch);
       }

@@ -45,6 +45,7 @@ struct Handle {
   float last_kernel_ms = 0.f;
   std::vector<std::vector<uint32_t>> keep;  // host sources of async uploads, alive until the create() sync
   int variant = 0;  // 0: k_run (lane per env); v > 0: k_wave shape kVariants[v] (see choose_variant)
+  std::string variant_note;  // why a device handle runs k_run ("" when k_wave, or when chosen explicitly)
   // host copies of the map fields the partitioned mode lays out its owned Q blocks with
   std::vector<uint8_t> h_sw_np, h_q_w;
   std::vector<uint64_t> h_q_off;
@@ -90,13 +91,18 @@ constexpr WaveShape kVariants[] = {{0, 0, 0}, {1, 1, 32}, {4, 1, 32}, {4, 1, 64}
 constexpr int kNumVariants = 6;
 
 // Eligibility: trains fit one or two slots per lane (T <= 128), the env fits the variant's
-// registers and every semaphore time fits the 11-bit register field.  SFL_KERNEL=scalar
-// forces k_run.
-inline int choose_variant(const sfl_map_desc* md, bool backend_has_wave) {
+// registers and every semaphore record fits the 32-bit LDS word (sfl_wave.h r_pack: start tick
+// -8192..8191, span <= 511).  SFL_KERNEL=scalar forces k_run.  why: when non-null, the reason a
+// map is not eligible (the caller reports it; the lane-per-env body is 15-45x slower).
+inline int choose_variant(const sfl_map_desc* md, bool backend_has_wave, std::string* why = nullptr) {
   if (!backend_has_wave) return 0;
   const char* env = getenv("SFL_KERNEL");
   if (env && strcmp(env, "scalar") == 0) return 0;
-  if (md->T > 128) return 0;
+  auto no = [&](const char* r) {
+    if (why) *why = r;
+    return 0;
+  };
+  if (md->T > 128) return no("more than 128 trains");
   int32_t ed_max = 0, ed_min = 0, dist_max = 0, len_max = 0;
   for (int32_t h = 0; h < md->T; ++h) {
     ed_max = md->tr_ed[h] > ed_max ? md->tr_ed[h] : ed_max;
@@ -106,12 +112,14 @@ inline int choose_variant(const sfl_map_desc* md, bool backend_has_wave) {
   for (int32_t p = 0; p < md->S * 4; ++p) len_max = md->port_len[p] > len_max ? md->port_len[p] : len_max;
   const int64_t span = (int64_t)(dist_max > 2 * len_max + 2 ? dist_max : 2 * len_max + 2) + 4;
   const int64_t t_hi = (int64_t)(ed_max > md->max_episode_steps ? ed_max : md->max_episode_steps) + 2 + span;
-  if (t_hi > 1023 || ed_min - 2 < -1024) return 0;
-  if (md->q_per_env >= (1ull << 32) || (int64_t)md->H * md->W >= (1 << 20) - 1) return 0;
+  if (t_hi > 8191 || ed_min - 2 < -8192) return no("timetable horizon beyond 8191 ticks");
+  if (span > 511) return no("a semaphore span beyond 511 ticks");
+  if (md->q_per_env >= (1ull << 32)) return no("Q-table beyond 2^32 cells per env");
+  if ((int64_t)md->H * md->W >= (1 << 20) - 1) return no("grid beyond 2^20 cells");
   for (int v = 1; v < kNumVariants; ++v) {
     if (md->S * 4 <= 64 * kVariants[v].PPL && md->S <= 64 * kVariants[v].SPL && md->T <= kVariants[v].TW) return v;
   }
-  return 0;
+  return no("more than 256 switches");
 }
 
 template <class B>
@@ -132,7 +140,7 @@ int create(const sfl_map_desc* md, const sfl_hparams* hp, uint32_t n_envs, const
   h->h_q_w.assign(md->q_w, md->q_w + (size_t)md->S * 4);
   h->h_q_off.assign(md->q_off, md->q_off + (size_t)md->S * 4);
   h->h_row_base.assign(md->row_base, md->row_base + (size_t)md->S * 4);
-  h->variant = choose_variant(md, B::kHasWave);
+  h->variant = choose_variant(md, B::kHasWave, &h->variant_note);
   SflMap& m = h->map;
   const size_t HW = (size_t)md->H * md->W, NP = (size_t)md->S * 4, S = md->S, T = md->T;
   m.H = md->H;
@@ -464,9 +472,9 @@ int scan_errors(Handle<B>* h) {
   if (h->be.sync()) return fail(h->be.error());
   for (uint32_t e = 0; e < h->E; ++e)
     if (err[e]) {
-      char buf[160];
+      char buf[256];
       snprintf(buf, sizeof buf, "env %u: error flags 0x%x (1=inf distance, 2=plan overflow, 4=port mismatch, 8=bad action, "
-               "16=message segment overflow)",
+               "16=message segment overflow, 32=decayed lr beyond the ntab table: raise ntab)",
                e, err[e]);
       return fail(buf);
     }

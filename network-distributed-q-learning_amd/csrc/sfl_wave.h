@@ -99,16 +99,22 @@ __device__ __forceinline__ uint32_t rl(uint32_t v, int lane) {
 }
 __device__ __forceinline__ int32_t rl(int32_t v, int lane) { return (int32_t)__builtin_amdgcn_readlane((int)v, lane); }
 
-// semaphore record in a VGPR: t0 11 | t1 11 | owner 8 | in 1 | present 1
+// semaphore record in a VGPR / LDS word: t0 14 (signed) | t1 - t0 9 | owner 7 | in 1 | present 1
+// (ticks -8192..8191 and spans up to 511: choose_variant checks the map's timetable and port lengths)
+constexpr uint32_t R_T0_BITS = 14, R_DUR_BITS = 9, R_OWNER_SHIFT = R_T0_BITS + R_DUR_BITS;
+constexpr uint32_t R_T0_MASK = (1u << R_T0_BITS) - 1u, R_DUR_MASK = (1u << R_DUR_BITS) - 1u;
 __device__ __forceinline__ uint32_t r_pack(uint32_t owner, uint32_t in, int32_t t0, int32_t t1) {
-  return ((uint32_t)t0 & 0x7FFu) | (((uint32_t)t1 & 0x7FFu) << 11) | ((owner & 0xFFu) << 22) | ((in & 1u) << 30) |
-         (1u << 31);
+  return ((uint32_t)t0 & R_T0_MASK) | (((uint32_t)(t1 - t0) & R_DUR_MASK) << R_T0_BITS) | ((owner & 0x7Fu) << R_OWNER_SHIFT) |
+         ((in & 1u) << 30) | (1u << 31);
 }
 __device__ __forceinline__ bool r_present(uint32_t r) { return (r >> 31) != 0u; }
 __device__ __forceinline__ uint32_t r_in(uint32_t r) { return (r >> 30) & 1u; }
-__device__ __forceinline__ uint32_t r_owner(uint32_t r) { return (r >> 22) & 0xFFu; }
-__device__ __forceinline__ int32_t r_t0(uint32_t r) { return ((int32_t)(r << 21)) >> 21; }
-__device__ __forceinline__ int32_t r_t1(uint32_t r) { return ((int32_t)(r << 10)) >> 21; }
+__device__ __forceinline__ uint32_t r_owner(uint32_t r) { return (r >> R_OWNER_SHIFT) & 0x7Fu; }
+__device__ __forceinline__ int32_t r_t0(uint32_t r) { return ((int32_t)(r << (32 - R_T0_BITS))) >> (32 - R_T0_BITS); }
+__device__ __forceinline__ uint32_t r_dur(uint32_t r) { return (r >> R_T0_BITS) & R_DUR_MASK; }
+__device__ __forceinline__ int32_t r_t1(uint32_t r) { return r_t0(r) + (int32_t)r_dur(r); }
+// the same record restarted at tick t (extend_semaphores: span kept)
+__device__ __forceinline__ uint32_t r_retime(uint32_t r, int32_t t) { return (r & ~R_T0_MASK) | ((uint32_t)t & R_T0_MASK); }
 __device__ __forceinline__ uint32_t r_from64(uint64_t x) {
   return sem_present(x) ? r_pack(sem_owner(x), sem_in(x), sem_t0(x), sem_t1(x)) : 0u;
 }
@@ -405,8 +411,8 @@ struct WEnv {
   // inside its [t0, t1] window, and of the opposite direction or owned by a malfunctioning train
   __device__ __forceinline__ uint32_t rec_blocks(uint32_t r, uint32_t h, Mask malf, uint32_t io) const {
     const uint32_t ow = r_owner(r);
-    const uint32_t win = (uint32_t)(~((now - r_t0(r)) | (r_t1(r) - now))) >> 31;
-    const uint32_t other = ((ow ^ h) + 0xFFu) >> 8;
+    const uint32_t win = (uint32_t)(now - r_t0(r)) <= r_dur(r) ? 1u : 0u;  // t0 <= now <= t1
+    const uint32_t other = ((ow ^ h) + 0x7Fu) >> 7;  // owner != h (both < 128)
     const uint32_t mf = mbit(malf, (int)ow) ? 1u : 0u;
     return (r >> 31) & win & other & ((r_in(r) ^ io ^ 1u) | mf);
   }
@@ -481,13 +487,18 @@ struct WEnv {
     __hip_atomic_fetch_or((SFL_AS_G uint32_t*)touchb + (row >> 5), 1u << (row & 31u), __ATOMIC_RELAXED,
                           __HIP_MEMORY_SCOPE_AGENT);
   }
-  __device__ __forceinline__ double lr_of(uint32_t n) const {
+  // (a decaying lr past the table is an error, E_LR_TABLE: see SflEnv::lr_of in sfl_core.h)
+  __device__ __forceinline__ double lr_of(uint32_t n) {
     if (m.lr_decay == 1.0) return m.lr0;  // lr0 * 1.0**n (distr_q.py:70-79)
-    return n < (uint32_t)m.ntab ? ldc(m.lr_tab, (size_t)n) : m.lr0 * pow_ool(m.lr_decay, (double)n);
+    if (n < (uint32_t)m.ntab) return ldc(m.lr_tab, (size_t)n);
+    lerr |= E_LR_TABLE;
+    return m.lr0;
   }
-  __device__ __forceinline__ double lr_of_var(uint32_t n) const {
+  __device__ __forceinline__ double lr_of_var(uint32_t n) {
     if (m.lr_decay == 1.0) return m.lr0;
-    return n < (uint32_t)m.ntab ? ld(m.lr_tab, (size_t)n) : m.lr0 * pow_ool(m.lr_decay, (double)n);
+    if (n < (uint32_t)m.ntab) return ld(m.lr_tab, (size_t)n);
+    lerr |= E_LR_TABLE;
+    return m.lr0;
   }
 
   // ---- launch-boundary state transfer ---------------------------------------------------------
@@ -574,7 +585,7 @@ struct WEnv {
     }
     uint32_t err = 0;
 #pragma unroll
-    for (int b = 0; b < (PART ? 5 : 4); ++b)
+    for (int b = 0; b < 6; ++b)
       if (__ballot((lerr >> b) & 1u)) err |= 1u << b;
     if (lane == 0) {
       st(s.phase, e, phase);
@@ -917,7 +928,7 @@ struct WEnv {
       for (int k = 0; k < PPL; ++k) {
         const uint32_t r = sem(k);
         const bool ext = r_present(r) & mbit(SM, (int)r_owner(r));
-        sem(k) = ext ? r_pack(r_owner(r), r_in(r), t, t + (r_t1(r) - r_t0(r))) : r;
+        sem(k) = ext ? r_retime(r, t) : r;
       }
     }
     Mask MA = mballot<TPL>(map_);

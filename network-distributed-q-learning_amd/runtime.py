@@ -80,6 +80,18 @@ class Batch:
                                                C.byref(handle)), "sfl_create")
         self.h = handle
         self._keep = []
+        note = C.create_string_buffer(256)
+        self.lib.check(self.lib.dll.sfl_get_kernel_note(self.h, note, 256), "sfl_get_kernel_note")
+        self.kernel_note = note.value.decode()
+        if self.kernel_note:
+            # the lane-per-env body is 15-45x slower than k_wave: say so, or refuse when asked to
+            import os
+            import warnings
+            msg = f"this map runs the lane-per-env kernel (k_run), not k_wave: {self.kernel_note}"
+            if os.environ.get("SFL_REQUIRE_WAVE") == "1":
+                self.close()
+                raise _lib.SflError(msg)
+            warnings.warn(msg, RuntimeWarning, stacklevel=2)
         self.learn_calls = 0
         self.trace_env = None
         self.trace_cap = 1 << 16

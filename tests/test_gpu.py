@@ -52,7 +52,7 @@ def test_golden_env0_and_trace(lib, kernel, name):
     cm = comp.compile_scenario(g["scenario_obj"])
     seed1 = g["seed"] + 7
     b = runtime.Batch(cm, hp, [g["seed"], seed1, seed1 + 1], lib=lib, max_steps=hp.get("max_steps", 100_000),
-                      ntab=4096)
+                      ntab=1 << 16)
     b.trace_env = 1
     _check_kernel(b, kernel)
     out = b.learn(g["n_episodes"], exploit_freq=g["exploit_freq"])
@@ -301,9 +301,10 @@ def test_c2_stated_batch_4096(lib):
 
 
 def test_device_pow_beyond_tables(lib, kernel):
-    """ntab = 16: epsilon and lr beyond the host tables come from the device's pow (pow_ool), with
-    decaying epsilon AND lr, checked against the oracle's Python ``**`` (distr_q.py:59-79)."""
-    hp = dict(gamma=0.95, epsilon=0.3, epsilon_decay_rate=0.99, lr=0.2, lr_decay_rate=0.999, default_q=-5.0)
+    """ntab = 16: epsilon beyond the host table comes from the device's pow (pow_ool); checked
+    against the oracle's Python ``**`` (distr_q.py:59-68) bit-exactly.  (eps only decides
+    ``random() < eps``: an ulp of pow moves that decision by ~1e-17 in probability.)"""
+    hp = dict(gamma=0.95, epsilon=0.3, epsilon_decay_rate=0.99, lr=0.2, lr_decay_rate=1.0, default_q=-5.0)
     sc = mapgen.make_config("c2")
     cm = comp.compile_scenario(sc)
     seeds = [77 + i for i in range(128)]
@@ -317,6 +318,21 @@ def test_device_pow_beyond_tables(lib, kernel):
         st = so.run_decisions(model, 900)
         assert max(st["counts"].values()) > 16  # the pow path ran
         assert b.q_dict(e) == model.q, f"env {e}"
+    b.close()
+
+
+def test_decayed_lr_beyond_table_fails_loudly(lib, kernel):
+    """A decaying lr (distr_q.py:70-79) enters the Q values, and the device pow differs from the
+    host libm's by an ulp (measured: round 2, test_device_pow_beyond_tables with lr_decay 0.999 at
+    ntab 16): past the table the run stops with E_LR_TABLE instead of silently losing bit-exactness."""
+    hp = dict(gamma=0.95, epsilon=0.3, epsilon_decay_rate=0.99, lr=0.2, lr_decay_rate=0.999, default_q=-5.0)
+    cm = comp.compile_scenario(mapgen.make_config("c2"))
+    b = runtime.Batch(cm, hp, [77, 78], lib=lib, ntab=16)
+    _check_kernel(b, kernel)
+    b.learn_begin()
+    b.apply_qinit()
+    with pytest.raises(_lib.SflError, match="ntab"):
+        b.step(900)
     b.close()
 
 
@@ -343,3 +359,46 @@ def test_distr_q_checkpoint_every_episode_gpu(lib, tmp_path, exploit):
 def test_distr_q_load_reference_pickle_gpu(lib, tmp_path):
     from tests import test_api_hostsim as api
     api.test_load_reference_pickle_format(tmp_path, lib=lib)
+
+
+def test_long_horizon_city_map_stays_on_wave(lib):
+    """A city map whose timetable horizon (t_hi = 1,110 ticks) overflowed round 1's 11-bit record
+    time field now runs k_wave (14-bit start tick, 9-bit span), bit-equal to the host build."""
+    from tests import hostsim
+    sc = mapgen.generate_cities(6, 24, seed=3, spacing=70, malfunction=(0.01, 5, 15), name="long")
+    assert sc.max_episode_steps > 900
+    cm = comp.compile_scenario(sc)
+    seeds = [900 + i for i in range(64)]
+    bg = runtime.Batch(cm, HP, seeds, lib=lib, ntab=1 << 14)
+    assert bg.counters()["kernel_variant"] > 0 and bg.kernel_note == ""
+    bh = runtime.Batch(cm, HP, seeds, lib=hostsim.lib(), ntab=1 << 14)
+    for b in (bg, bh):
+        b.learn_begin()
+        b.apply_qinit()
+        for n in (300, 900):
+            b.step(n)
+    for e in range(len(seeds)):
+        qg, tg = bg.q_raw(e)
+        qh, th = bh.q_raw(e)
+        assert np.array_equal(qg, qh) and np.array_equal(tg, th), f"env {e}"
+        sg, sh = _env_state(bg, e), _env_state(bh, e)
+        assert sg[0] == sh[0] and all(np.array_equal(x, y) for x, y in zip(sg[2:], sh[2:])), f"env {e}"
+    env, model = so.build(sc, seeds[7], HP, trace=False)
+    so.run_decisions(model, 1200)
+    assert bg.q_dict(7) == model.q
+    bg.close()
+    bh.close()
+
+
+def test_fallback_kernel_is_reported(lib, monkeypatch):
+    """A map k_wave cannot hold (more than 256 switches) runs the lane-per-env body with a
+    warning, or is refused under SFL_REQUIRE_WAVE=1."""
+    sc = mapgen.generate(300, 40, 8, seed=5, name="big")
+    cm = comp.compile_scenario(sc)
+    with pytest.warns(RuntimeWarning, match="256 switches"):
+        b = runtime.Batch(cm, HP, [1, 2], lib=lib)
+    assert b.counters()["kernel_variant"] == 0
+    b.close()
+    monkeypatch.setenv("SFL_REQUIRE_WAVE", "1")
+    with pytest.raises(_lib.SflError, match="256 switches"):
+        runtime.Batch(cm, HP, [1, 2], lib=lib)
