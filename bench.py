@@ -181,7 +181,7 @@ def main():
     abytes = 0
     dec_l = ticks_l = 0
     cnt0 = b.counters()
-    kname = (f"k_wave<{cnt0['kernel_variant']}> (one env per wavefront)" if cnt0["kernel_variant"] > 0
+    kname = (f"k_wave<{cnt0['kernel_variant']}> ({64 // cnt0['group_lanes']} env(s) per wavefront)" if cnt0["kernel_variant"] > 0
              else "k_run (one env per lane)")
     for _ in range(args.steps):
         n, ms = b.step(args.decisions)

@@ -39,6 +39,15 @@ __global__ void __launch_bounds__(SFL_WAVE_BLOCK) __attribute__((amdgpu_waves_pe
                                               const sfl::SflCtl* __restrict__ c) {
   sfl::wave::run<PPL, SPL, TW, TRACE>(*m, *s, *c);
 }
+// several envs per wavefront (sfl_wave.h run_groups): G lanes per env, SFL_WAVE_BLOCK / G envs per block
+#ifndef SFL_GROUP_OCC
+#define SFL_GROUP_OCC 3  // waves per SIMD the grouped kernel is register-budgeted for (c3 at G = 16: LDS allows 3)
+#endif
+template <int PPL, int SPL, int TW, bool TRACE, int G>
+__global__ void __launch_bounds__(SFL_WAVE_BLOCK) __attribute__((amdgpu_waves_per_eu(SFL_GROUP_OCC)))
+k_wave_g(const sfl::SflMap* __restrict__ m, const sfl::SflState* __restrict__ s, const sfl::SflCtl* __restrict__ c) {
+  sfl::wave::run_groups<PPL, SPL, TW, TRACE, G>(*m, *s, *c);
+}
 // maps with 65-128 trains (two train slots per lane): one env per 64-thread block (its LDS is
 // ~22 KB), register budget for the LDS-bound occupancy of 2 waves per SIMD
 #ifndef SFL_WAVE2_OCC
@@ -284,12 +293,24 @@ struct HipBackend {
 #define SFL_KW2(v)                                                                                       \
   (c.trace ? k_wave2<sfl::kVariants[v].PPL, sfl::kVariants[v].SPL, sfl::kVariants[v].TW, true><<<s.E, 64, 0, stream>>>(pm, ps, pc) \
            : k_wave2<sfl::kVariants[v].PPL, sfl::kVariants[v].SPL, sfl::kVariants[v].TW, false><<<s.E, 64, 0, stream>>>(pm, ps, pc))
-    static_assert(sfl::kVariants[5].TW > 64 && sfl::kNumVariants == 6, "variant 5 is the two-slot shape");
+#define SFL_KG(v)                                                                                               \
+  {                                                                                                             \
+    constexpr sfl::WaveShape w = sfl::kVariants[v];                                                             \
+    const unsigned gblocks = (unsigned)(((size_t)s.E * w.G + SFL_WAVE_BLOCK - 1) / SFL_WAVE_BLOCK);             \
+    if (c.trace) k_wave_g<w.PPL, w.SPL, w.TW, true, w.G><<<gblocks, SFL_WAVE_BLOCK, 0, stream>>>(pm, ps, pc);    \
+    else k_wave_g<w.PPL, w.SPL, w.TW, false, w.G><<<gblocks, SFL_WAVE_BLOCK, 0, stream>>>(pm, ps, pc);          \
+  }
+    static_assert(sfl::kVariants[5].TW > 64 && sfl::kNumVariants == 10, "variant 5 is the two-slot shape, 6-9 grouped");
     if (variant == 1) SFL_KW(1);
     else if (variant == 2) SFL_KW(2);
     else if (variant == 3) SFL_KW(3);
     else if (variant == 4) SFL_KW(4);
     else if (variant == 5) SFL_KW2(5);
+    else if (variant == 6) SFL_KG(6)
+    else if (variant == 7) SFL_KG(7)
+    else if (variant == 8) SFL_KG(8)
+    else if (variant == 9) SFL_KG(9)
+#undef SFL_KG
 #undef SFL_KW2
 #undef SFL_KW
     else if (m.T <= 32) k_run<1><<<blocks, 256, 0, stream>>>(pm, ps, pc);

@@ -84,11 +84,16 @@ struct Handle {
 // One-env-per-wavefront kernel shapes (sfl_wave.h): PPL semaphore and SPL counter registers
 // per lane (ports <= 64*PPL, switches <= 64*SPL).  Index 0 = the lane-per-env kernel (k_run).
 // TW: trains per env the variant's LDS prefetch records are sized for (T <= TW).
+// G: lanes per env (64: one env per wavefront; 32 / 16: two / four envs per wavefront, run_groups).
 struct WaveShape {
-  int PPL, SPL, TW;
+  int PPL, SPL, TW, G;
 };
-constexpr WaveShape kVariants[] = {{0, 0, 0}, {1, 1, 32}, {4, 1, 32}, {4, 1, 64}, {8, 2, 64}, {16, 4, 128}};
-constexpr int kNumVariants = 6;
+constexpr WaveShape kVariants[] = {{0, 0, 0, 64},   {1, 1, 32, 64},  {4, 1, 32, 64}, {4, 1, 64, 64}, {8, 2, 64, 64},
+                                   {16, 4, 128, 64}, {4, 1, 16, 16},  {16, 4, 32, 16}, {2, 1, 32, 32}, {8, 2, 32, 32}};
+constexpr int kNumVariants = 10;
+#ifndef SFL_DEFAULT_G
+#define SFL_DEFAULT_G 64  // lane group size chosen where a grouped shape fits (SFL_WAVE_G overrides)
+#endif
 
 // Eligibility: trains fit one or two slots per lane (T <= 128), the env fits the variant's
 // registers and every semaphore record fits the 32-bit LDS word (sfl_wave.h r_pack: start tick
@@ -114,12 +119,30 @@ inline int choose_variant(const sfl_map_desc* md, bool backend_has_wave, std::st
   const int64_t t_hi = (int64_t)(ed_max > md->max_episode_steps ? ed_max : md->max_episode_steps) + 2 + span;
   if (t_hi > 8191 || ed_min - 2 < -8192) return no("timetable horizon beyond 8191 ticks");
   if (span > 511) return no("a semaphore span beyond 511 ticks");
+  for (size_t i = 0, n = (size_t)md->K * md->H * md->W * 4; i < n; ++i)  // (staged as int16, sfl_wave.h d16)
+    if (md->dist[i] >= 32767 && md->dist[i] < DIST_INF) return no("a finite distance of 32767 cells or more");
   if (md->q_per_env >= (1ull << 32)) return no("Q-table beyond 2^32 cells per env");
   if ((int64_t)md->H * md->W >= (1 << 20) - 1) return no("grid beyond 2^20 cells");
-  for (int v = 1; v < kNumVariants; ++v) {
-    if (md->S * 4 <= 64 * kVariants[v].PPL && md->S <= 64 * kVariants[v].SPL && md->T <= kVariants[v].TW) return v;
-  }
+  const char* gs = getenv("SFL_WAVE_G");
+  const int want_g = gs ? atoi(gs) : SFL_DEFAULT_G;
+  auto fits = [&](int v) {
+    const WaveShape& w = kVariants[v];
+    return md->S * 4 <= w.G * w.PPL && md->S <= w.G * w.SPL && md->T <= w.TW;
+  };
+  for (int v = 1; v < kNumVariants; ++v)
+    if (kVariants[v].G == want_g && fits(v)) return v;
+  for (int v = 1; v < kNumVariants; ++v)
+    if (kVariants[v].G == 64 && fits(v)) return v;
   return no("more than 256 switches");
+}
+
+// the one-env-per-wavefront shape of the same map (the partitioned local step runs G = 64 only)
+inline int wave64_variant(int S, int T) {
+  for (int v = 1; v < kNumVariants; ++v) {
+    const WaveShape& w = kVariants[v];
+    if (w.G == 64 && S * 4 <= w.G * w.PPL && S <= w.G * w.SPL && T <= w.TW) return v;
+  }
+  return 0;
 }
 
 template <class B>
@@ -625,6 +648,8 @@ int part_config(Handle<B>* h, int rank, int world, const int32_t* owner, uint32_
   h->be.fill_f64(P.q_own, h->map.default_q, (size_t)E_tot * off);
   h->be.memset(P.touched_own, 0, (size_t)E_tot * P.own_words * 4);
   h->be.memset(P.dec_done, 0, h->E * 8);
+  // a grouped shape (G < 64) becomes its one-env-per-wavefront shape: same env-major state layout
+  if (h->variant > 0 && kVariants[h->variant].G != 64) h->variant = wave64_variant(h->map.S, h->map.T);
   // the partitioned rounds run the body the handle was created for (h->variant: k_wave where
   // eligible, else the lane-per-env body), with that body's (switch, train) slot layout
   return h->be.sync() ? fail(h->be.error()) : 0;

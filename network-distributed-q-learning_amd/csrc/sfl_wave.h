@@ -17,6 +17,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "sfl_core.h"
 #include "sfl_part.h"
 
@@ -51,7 +53,21 @@ constexpr uint32_t PF_NONE = 0xFFFFFFFFu;
 // projected cell if it stops (reward of STOP), if it moves with final rail action 0..3 (reward of
 // a route), and the row's argmax | first allowed argmax << 8 under the staged observation (the
 // row's columns themselves are not kept: a decision on a staged row needs only its max and argmaxes)
-constexpr int PF_W = 7, PF_I = 6;
+constexpr int PF_W = 5, PF_I = 6;
+// (the layout, in 32-bit words: 0-1 pending cell value, 2-3 slot word, 4-5 row max; 6: distance at the
+// cell | along the STOP plan << 16, 7: route final action 1 | 2 << 16, 8: route final action 3 |
+// argmax pack << 16 (int16 distances, see d16); 9: spare)
+// distances staged as int16: off the grid -> INT16_MIN, unreachable -> INT16_MAX (choose_variant
+// checks that every finite distance of the map is below 32767)
+__device__ __forceinline__ uint32_t d16(int32_t d) {
+  const int32_t v = d == (int32_t)0x80000000 ? -32768 : (d >= 32767 ? 32767 : d);
+  return (uint32_t)v & 0xFFFFu;
+}
+__device__ __forceinline__ int32_t d16_lo(uint32_t w) {
+  const int32_t v = (int32_t)(int16_t)(w & 0xFFFFu);
+  return v == -32768 ? (int32_t)0x80000000 : (v == 32767 ? DIST_INF : v);
+}
+__device__ __forceinline__ int32_t d16_hi(uint32_t w) { return d16_lo(w >> 16); }
 #ifndef SFL_WAVE_BLOCK
 #define SFL_WAVE_BLOCK 256  // threads per k_wave block (envs per block x 64)
 #endif
@@ -167,20 +183,11 @@ __device__ __forceinline__ uint64_t mfirst(uint64_t, int n) { return n >= 64 ? ~
 __device__ __forceinline__ M2 mfirst(M2, int n) {
   return n >= 128 ? M2{{~0ull, ~0ull}} : n >= 64 ? M2{{~0ull, (n == 64) ? 0ull : (1ull << (n - 64)) - 1ull}} : M2{{(1ull << n) - 1ull, 0ull}};
 }
-template <int TPL>
+// train masks: one 64-bit word for up to 64 trains, two (M2) for up to 128
+template <int BITS>
 struct MaskOf {
-  using type = uint64_t;
+  using type = typename std::conditional<(BITS <= 64), uint64_t, M2>::type;
 };
-template <>
-struct MaskOf<2> {
-  using type = M2;
-};
-// one ballot per train slot
-template <int TPL>
-__device__ __forceinline__ typename MaskOf<TPL>::type mballot(const bool (&p)[TPL]) {
-  if constexpr (TPL == 1) return __ballot(p[0]);
-  else return M2{{__ballot(p[0]), __ballot(p[1])}};
-}
 
 // max over each quad of lanes (DPP quad permutes; the result is valid in every lane of the quad)
 template <int CTRL>
@@ -219,22 +226,34 @@ struct PortRec {
   __device__ __forceinline__ uint32_t row_base() const { return w[2]; }
   __device__ __forceinline__ uint32_t q_off() const { return w[3]; }
 };
-// PPL semaphore registers (ports <= 64*PPL) and SPL counter registers (switches <= 64*SPL) per lane
-// PART: the graph-partitioned mode's local step (sfl_part.h): the env's Q rows live on their
-// switches' owner ranks, so a decision is observed in one launch (request to the owner) and
+// G lanes per env (a lane group; G = 64: one env per wavefront, G = 32 / 16: two / four envs per
+// wavefront, for maps with few trains).  PPL semaphore words (ports <= G*PPL) and SPL counter words
+// (switches <= G*SPL) per lane.  With G = 64 the env's control values are wave-uniform and live in
+// SGPRs (uni, readlane, ballot, scalar loads of the map tables); with G < 64 they are group-uniform
+// VGPRs: a cross-lane read is a ds_bpermute inside the group, a ballot is the group's slice of the
+// wave's, and the map tables are read with vector loads (the groups of a wave sit on different
+// switches).  Branches on group-uniform values diverge across the groups of a wave, which the
+// flat loop of run_groups (one tick / post / decision per group and iteration) keeps balanced.
+// PART: the graph-partitioned mode's local step (sfl_part.h, G = 64 only): the env's Q rows live on
+// their switches' owner ranks, so a decision is observed in one launch (request to the owner) and
 // applied in the next (with the owner's reply), and the post step's Q operations are update
 // records to the owners
-template <int PPL, int SPL, int TWc, bool PART = false>
+template <int PPL, int SPL, int TWc, bool PART = false, int G = 64>
 struct WEnv {
+  static_assert(G == 64 || G == 32 || G == 16, "lane group of 16, 32 or 64 lanes");
+  static_assert(G == 64 || !PART, "the partitioned local step runs one env per wavefront");
   const SflMap& m;
   const SflState& s;
   const uint32_t e, E;
-  const int lane;
+  const int lane;   // lane in the env's group (0 .. G-1)
+  const int gbase;  // first wavefront lane of the group
   const SflPart* P;  // PART only
-  static constexpr int TPL = (TWc + 63) / 64;  // train slots per lane: trains lane, lane + 64
-  using Mask = typename MaskOf<TPL>::type;
-  bool mine[TPL];  // lane + 64 k < T: slot k holds train lane + 64 k
-  // the lane's trains (slot k = train lane + 64 k)
+  static constexpr int TPL = (TWc + G - 1) / G;  // train slots per lane: trains lane, lane + G, ...
+  static constexpr int kG = G;
+  static_assert(TPL * G <= 128, "at most 128 train slots per env");
+  using Mask = typename MaskOf<TPL * G>::type;
+  bool mine[TPL];  // lane + G k < T: slot k holds train lane + G k
+  // the lane's trains (slot k = train lane + G k)
   int32_t pos[TPL];
   uint32_t bits[TPL], plan[TPL];
   uint32_t nprv[TPL];  // next port | prev port << 16
@@ -277,15 +296,19 @@ struct WEnv {
   uint64_t lap_t = 0;
 #endif
 
-  __device__ WEnv(const SflMap& m_, const SflState& s_, uint32_t e_, int lane_, uint32_t* lds, const SflPart* P_ = nullptr)
-      : m(m_), s(s_), e(e_), E(s_.E), lane(lane_), P(P_), lsem(lds), lcnt(lds + 64 * PPL), lpf((double*)(lds + 64 * (PPL + SPL))) {
+  // lds: this env's region; ltt_shared: the block's copy of the timetable rows (G < 64), or null for
+  // the env's own copy after its region
+  __device__ WEnv(const SflMap& m_, const SflState& s_, uint32_t e_, int wlane, uint32_t* lds, const SflPart* P_ = nullptr,
+                  int32_t* ltt_shared = nullptr)
+      : m(m_), s(s_), e(e_), E(s_.E), lane(wlane & (G - 1)), gbase(wlane & ~(G - 1)), P(P_), lsem(lds), lcnt(lds + G * PPL),
+        lpf((double*)(lds + G * (PPL + SPL))) {
 #pragma unroll
     for (int k = 0; k < TPL; ++k) {
-      mine[k] = lane_ + 64 * k < m_.T;
+      mine[k] = lane + G * k < m_.T;
       pf_roff[k] = pf_qoff[k] = PF_NONE;
     }
-    lrng = (uint64_t*)(lds + 64 * (PPL + SPL) + TWc * PF_W * 2);
-    ltt = (const int32_t*)(lds + 64 * (PPL + SPL) + TWc * PF_W * 2 + 12);
+    lrng = (uint64_t*)(lds + G * (PPL + SPL) + TWc * PF_W * 2);
+    ltt = ltt_shared ? ltt_shared : (const int32_t*)(lds + G * (PPL + SPL) + TWc * PF_W * 2 + 12);
     qb = s.q + (size_t)e * m.q_per_env;
     pf_ok = false;
     touchb = s.touched + (size_t)e * m.touched_words;
@@ -301,13 +324,58 @@ struct WEnv {
   __device__ __forceinline__ size_t pix(int p) const { return (size_t)e * (uint32_t)m.NP + (uint32_t)p; }
   __device__ __forceinline__ size_t cix(int sw) const { return (size_t)e * (uint32_t)m.S + (uint32_t)sw; }
 
-  // ---- cross-lane access (index wave-uniform) -------------------------------------
-  __device__ __forceinline__ uint32_t sget(int p) const { return uni(lsem[p]); }
+  // ---- group primitives -------------------------------------------------------------
+  // a group-uniform value: in an SGPR for G = 64 (readfirstlane), as is for G < 64
+  template <class T>
+  __device__ __forceinline__ T U(T x) const {
+    if constexpr (G == 64) return uni(x);
+    else return x;
+  }
+  __device__ __forceinline__ double Ud(double x) const {
+    if constexpr (G == 64) return unid(x);
+    else return x;
+  }
+  // lane i of the group (i group-uniform)
+  __device__ __forceinline__ uint32_t RL(uint32_t v, int i) const {
+    if constexpr (G == 64) return rl(v, i);
+    else return (uint32_t)__builtin_amdgcn_ds_bpermute((gbase + i) << 2, (int)v);
+  }
+  __device__ __forceinline__ int32_t RL(int32_t v, int i) const { return (int32_t)RL((uint32_t)v, i); }
+  // the group's lanes with p set (bit i = lane i of the group)
+  __device__ __forceinline__ uint64_t BAL(bool p) const {
+    if constexpr (G == 64) return __ballot(p);
+    else return (__ballot(p) >> gbase) & ((1ull << G) - 1ull);
+  }
+  // one ballot per train slot: bit h = train h
+  __device__ __forceinline__ Mask mbal(const bool (&p)[TPL]) const {
+    if constexpr (TPL * G <= 64) {
+      uint64_t r = 0;
+#pragma unroll
+      for (int k = 0; k < TPL; ++k) r |= BAL(p[k]) << (G * k);
+      return r;
+    } else {
+      return M2{{BAL(p[0]), BAL(p[1])}};
+    }
+  }
+  // read-only map tables at a group-uniform index: scalar loads (K$) for G = 64, vector loads else
+  template <class T>
+  __device__ __forceinline__ T LDC(const T* p, size_t i) const {
+    if constexpr (G == 64) return ldc(p, i);
+    else return ld(p, i);
+  }
+  template <class V>
+  __device__ __forceinline__ V LDCV(const void* p, size_t i) const {
+    if constexpr (G == 64) return ldcv<V>(p, i);
+    else return ld((const V*)p, i);
+  }
+
+  // ---- cross-lane access (index group-uniform) --------------------------------------
+  __device__ __forceinline__ uint32_t sget(int p) const { return U(lsem[p]); }
   __device__ __forceinline__ void sset(int p, uint32_t r) {
     lsem[p] = r;  // wave-uniform value from every lane (one address): no lane-0 exec region
   }
-  __device__ __forceinline__ uint32_t& sem(int k) const { return lsem[k * 64 + lane]; }  // lane-parallel
-  __device__ __forceinline__ uint32_t cget(int sw) const { return uni(lcnt[sw]); }
+  __device__ __forceinline__ uint32_t& sem(int k) const { return lsem[k * G + lane]; }  // lane-parallel
+  __device__ __forceinline__ uint32_t cget(int sw) const { return U(lcnt[sw]); }
   __device__ __forceinline__ void cset(int sw, uint32_t v) {
     lcnt[sw] = v;  // wave-uniform value from every lane
   }
@@ -315,13 +383,19 @@ struct WEnv {
   // train h's value of a per-train register (h wave-uniform)
   template <class T>
   __device__ __forceinline__ T trl(const T (&x)[TPL], int h) const {
-    if constexpr (TPL == 1) return rl(x[0], h);
-    else return rl((h & 64) ? x[1] : x[0], h & 63);
+    if constexpr (TPL == 1) {
+      return RL(x[0], h);
+    } else {
+      T v = x[0];
+#pragma unroll
+      for (int k = 1; k < TPL; ++k) v = (h / G == k) ? x[k] : v;
+      return RL(v, h & (G - 1));
+    }
   }
   template <class T>
   __device__ __forceinline__ void tset(T (&x)[TPL], int h, T v) {
 #pragma unroll
-    for (int k = 0; k < TPL; ++k) x[k] = (lane + 64 * k == h) ? v : x[k];
+    for (int k = 0; k < TPL; ++k) x[k] = (lane + G * k == h) ? v : x[k];
   }
   __device__ __forceinline__ uint32_t state_of(int h) const { return tb_state(trl(bits, h)); }
   // malfunctioning trains (check_port_blocked's owner test)
@@ -329,17 +403,17 @@ struct WEnv {
     bool p[TPL];
 #pragma unroll
     for (int k = 0; k < TPL; ++k) p[k] = mine[k] && tb_state(bits[k]) == S_MALF;
-    return mballot<TPL>(p);
+    return mbal(p);
   }
 
   // ---- map records --------------------------------------------------------------------
-  __device__ __forceinline__ SwRec sw_rec(int sw) const { return SwRec{ldcv<u8>(m.sw_pack, (size_t)sw * 2u)}; }
+  __device__ __forceinline__ SwRec sw_rec(int sw) const { return SwRec{LDCV<u8>(m.sw_pack, (size_t)sw * 2u)}; }
   // neighbour ports of the switch's ports 0-3 (16 bits each)
   __device__ __forceinline__ vec_t<uint32_t, 2> sw_nb(int sw) const {
-    return ldcv<vec_t<uint32_t, 2>>(m.sw_pack, (size_t)sw * 8u + 4u);
+    return LDCV<vec_t<uint32_t, 2>>(m.sw_pack, (size_t)sw * 8u + 4u);
   }
-  __device__ __forceinline__ PortRec port_rec(int p) const { return PortRec{ldcv<u4>(m.port_pack, (size_t)p)}; }
-  __device__ __forceinline__ int port_nb(int p) const { return (int)(int16_t)(ldc(m.port_pack, (size_t)p * 4) & 0xFFFFu); }
+  __device__ __forceinline__ PortRec port_rec(int p) const { return PortRec{LDCV<u4>(m.port_pack, (size_t)p)}; }
+  __device__ __forceinline__ int port_nb(int p) const { return (int)(int16_t)(LDC(m.port_pack, (size_t)p * 4) & 0xFFFFu); }
   struct Move {
     int cell, dir;
     bool valid, cell_ok;
@@ -360,14 +434,14 @@ struct WEnv {
     return mv.cell >= 0 ? (int)ld(m.cell_sw, (size_t)mv.cell) : -1;
   }
   // flatland-lite check_action_on_agent as a table lookup; U: wave-uniform arguments (scalar load)
-  template <bool U>
+  template <bool UNI>
   __device__ __forceinline__ Move check_action(uint32_t a, int cell, int dir) const {
     const uint32_t i = ((uint32_t)cell * 4u + (uint32_t)dir) * 4u + (a & 3u);
-    return unpack_move(U ? ldc(m.move_tab, i) : ld(m.move_tab, i));
+    return unpack_move(UNI ? LDC(m.move_tab, i) : ld(m.move_tab, i));
   }
-  template <bool U>
+  template <bool UNI>
   __device__ __forceinline__ bool action_ok(uint32_t a, int cell, int dir) const {
-    Move mv = check_action<U>(a, cell, dir);
+    Move mv = check_action<UNI>(a, cell, dir);
     return mv.cell_ok && mv.valid;
   }
   // distance map lookup (wave-uniform)
@@ -376,7 +450,7 @@ struct WEnv {
       lerr |= E_INF_DIST;
       return 0;
     }
-    const int32_t d = ldc(m.dist, ((uint32_t)k * (uint32_t)m.HW + (uint32_t)cell) * 4u + (uint32_t)dir);
+    const int32_t d = LDC(m.dist, ((uint32_t)k * (uint32_t)m.HW + (uint32_t)cell) * 4u + (uint32_t)dir);
     if (d >= DIST_INF) lerr |= E_INF_DIST;
     return d;
   }
@@ -490,7 +564,7 @@ struct WEnv {
   // (a decaying lr past the table is an error, E_LR_TABLE: see SflEnv::lr_of in sfl_core.h)
   __device__ __forceinline__ double lr_of(uint32_t n) {
     if (m.lr_decay == 1.0) return m.lr0;  // lr0 * 1.0**n (distr_q.py:70-79)
-    if (n < (uint32_t)m.ntab) return ldc(m.lr_tab, (size_t)n);
+    if (n < (uint32_t)m.ntab) return LDC(m.lr_tab, (size_t)n);
     lerr |= E_LR_TABLE;
     return m.lr0;
   }
@@ -505,7 +579,7 @@ struct WEnv {
   __device__ __forceinline__ void load() {
 #pragma unroll
     for (int k = 0; k < TPL; ++k) {
-      const int hk = lane + 64 * k;
+      const int hk = lane + G * k;
       if (mine[k]) {
         pos[k] = ld(s.tr_pos, tix(hk));
         bits[k] = ld(s.tr_bits, tix(hk));
@@ -526,24 +600,24 @@ struct WEnv {
     }
 #pragma unroll
     for (int k = 0; k < PPL; ++k) {
-      const int p = k * 64 + lane;
+      const int p = k * G + lane;
       sem(k) = p < m.NP ? r_from64(ld(s.sem, pix(p))) : 0u;
     }
 #pragma unroll
     for (int k = 0; k < SPL; ++k) {
-      const int sw = k * 64 + lane;
-      lcnt[k * 64 + lane] = sw < m.S ? ld(s.counts, cix(sw)) : 0u;
+      const int sw = k * G + lane;
+      lcnt[k * G + lane] = sw < m.S ? ld(s.counts, cix(sw)) : 0u;
     }
-    now = uni(ld(s.elapsed, e));
-    flags = uni(ld(s.eflags, e));
-    epoch = uni(ld(s.epoch, e));
-    lerr = uni(ld(s.err, e));
+    now = U(ld(s.elapsed, e));
+    flags = U(ld(s.eflags, e));
+    epoch = U(ld(s.epoch, e));
+    lerr = U(ld(s.err, e));
     auto word = [&](int k, int w) {
-      return uni((uint64_t)ld(s.masks, (size_t)(k * MAXW + 2 * w) * E + e) |
+      return U((uint64_t)ld(s.masks, (size_t)(k * MAXW + 2 * w) * E + e) |
                  ((uint64_t)ld(s.masks, (size_t)(k * MAXW + 2 * w + 1) * E + e) << 32));
     };
     auto mask = [&](int k) -> Mask {
-      if constexpr (TPL == 1) return word(k, 0);
+      if constexpr (TPL * G <= 64) return word(k, 0);
       else return M2{{word(k, 0), word(k, 1)}};
     };
     q_mask = mask(0);
@@ -551,17 +625,17 @@ struct WEnv {
     fl_mask = mask(2);
     mf_mask = mask(3);
     if (lane < 5) lrng[lane] = ld(s.rng, ix((size_t)lane));
-    cum = (int64_t)unid(ld(s.cum_reward, e));
-    n_mf = uni(ld(s.n_mf, e));
-    ep_dec = uni(ld(s.ep_dec, e));
-    ep_ticks = uni(ld(s.ep_ticks, e));
-    step_ctr = (int32_t)uni(ld(s.step_ctr, e));
+    cum = (int64_t)Ud(ld(s.cum_reward, e));
+    n_mf = U(ld(s.n_mf, e));
+    ep_dec = U(ld(s.ep_dec, e));
+    ep_ticks = U(ld(s.ep_ticks, e));
+    step_ctr = (int32_t)U(ld(s.step_ctr, e));
     n_dec = 0;
   }
   __device__ __forceinline__ void store(int32_t phase) {
 #pragma unroll
     for (int k = 0; k < TPL; ++k) {
-      const int hk = lane + 64 * k;
+      const int hk = lane + G * k;
       if (mine[k]) {
         st(s.tr_pos, tix(hk), pos[k]);
         st(s.tr_bits, tix(hk), bits[k]);
@@ -575,18 +649,18 @@ struct WEnv {
     }
 #pragma unroll
     for (int k = 0; k < PPL; ++k) {
-      const int p = k * 64 + lane;
+      const int p = k * G + lane;
       if (p < m.NP) st(s.sem, pix(p), r_to64(sem(k)));
     }
 #pragma unroll
     for (int k = 0; k < SPL; ++k) {
-      const int sw = k * 64 + lane;
-      if (sw < m.S) st(s.counts, cix(sw), lcnt[k * 64 + lane]);
+      const int sw = k * G + lane;
+      if (sw < m.S) st(s.counts, cix(sw), lcnt[k * G + lane]);
     }
     uint32_t err = 0;
 #pragma unroll
     for (int b = 0; b < 6; ++b)
-      if (__ballot((lerr >> b) & 1u)) err |= 1u << b;
+      if (BAL((lerr >> b) & 1u)) err |= 1u << b;
     if (lane == 0) {
       st(s.phase, e, phase);
       st(s.elapsed, e, now);
@@ -595,7 +669,8 @@ struct WEnv {
       st(s.err, e, err);
       auto put = [&](int k, const Mask& mk) {
         uint64_t w[2];
-        if constexpr (TPL == 1) {
+        constexpr int NWD = TPL * G <= 64 ? 1 : 2;
+        if constexpr (NWD == 1) {
           w[0] = mk;
           w[1] = 0ull;
         } else {
@@ -603,7 +678,7 @@ struct WEnv {
           w[1] = mk.w[1];
         }
 #pragma unroll
-        for (int j = 0; j < 2 * TPL; ++j) st(s.masks, (size_t)(k * MAXW + j) * E + e, (uint32_t)(w[j >> 1] >> (32 * (j & 1))));
+        for (int j = 0; j < 2 * NWD; ++j) st(s.masks, (size_t)(k * MAXW + j) * E + e, (uint32_t)(w[j >> 1] >> (32 * (j & 1))));
       };
       put(0, q_mask);
       put(1, arr_mask);
@@ -627,7 +702,7 @@ struct WEnv {
 #pragma unroll
     for (int k = 0; k < TPL; ++k) {
       if (mine[k]) {
-        const int hk = lane + 64 * k;
+        const int hk = lane + G * k;
         const uint32_t t_init = (uint32_t)ltt[8 * hk + 7];
         pos[k] = -1;
         bits[k] = tb_make(t_init & 0xFFu, S_WAITING, A_NONE, 0, 0, 0);
@@ -639,7 +714,7 @@ struct WEnv {
 #pragma unroll
     for (int k = 0; k < PPL; ++k) sem(k) = 0u;
     for (int h = 0; h < m.T; ++h) {
-      const vec_t<int32_t, 8> tr = ldcv<vec_t<int32_t, 8>>(m.tr_pack, (size_t)h);
+      const vec_t<int32_t, 8> tr = LDCV<vec_t<int32_t, 8>>(m.tr_pack, (size_t)h);
       sset((int)((uint32_t)tr[7] >> 16), r_pack(h, 1, tr[0] - 2, tr[0] + tr[5]));
     }
     flags &= ~(F_TERM | F_TRUNC | F_OWN_SCAN | F_INFLIGHT);
@@ -647,7 +722,7 @@ struct WEnv {
     // new (switch, train) epoch: slots from older episodes read as empty
     epoch = (epoch + 1u) & 0xFFu;
     if (epoch == 0) {
-      for (int i = lane; i < m.S * m.T; i += 64) st(slotb, (size_t)i, slot_make(PEND_NONE, 0, 0));
+      for (int i = lane; i < m.S * m.T; i += G) st(slotb, (size_t)i, slot_make(PEND_NONE, 0, 0));
       epoch = 1;
     }
     cum = 0;
@@ -668,8 +743,8 @@ struct WEnv {
     vec_t<int32_t, 4> tt0[TPL], tt1[TPL];
 #pragma unroll
     for (int k = 0; k < TPL; ++k) {
-      tt0[k] = *(const vec_t<int32_t, 4>*)(ltt + 8 * (mine[k] ? lane + 64 * k : 0));
-      tt1[k] = *(const vec_t<int32_t, 4>*)(ltt + 8 * (mine[k] ? lane + 64 * k : 0) + 4);
+      tt0[k] = *(const vec_t<int32_t, 4>*)(ltt + 8 * (mine[k] ? lane + G * k : 0));
+      tt1[k] = *(const vec_t<int32_t, 4>*)(ltt + 8 * (mine[k] ? lane + G * k : 0) + 4);
     }
     // pass 1: plan pop + prediction, malfunction draw, action preprocessing, desired move
     bool mover[TPL];
@@ -677,7 +752,7 @@ struct WEnv {
     uint32_t aux[TPL];
 #pragma unroll
     for (int k = 0; k < TPL; ++k) {
-      const int h = lane + 64 * k;
+      const int h = lane + G * k;
       const int32_t t_init_cell = tt1[k][0];
       const uint32_t t_init_dir = (uint32_t)tt1[k][3] & 0xFFu;
       mover[k] = false;
@@ -758,7 +833,7 @@ struct WEnv {
     SFL_LAP(11);
     // pass 2: motion check, least fixed point (flatland_lite.motion_check): the lowest handle
     // wanting a cell wins it; a cell can be entered if free or its occupant moves out
-    const Mask M = mballot<TPL>(mover);
+    const Mask M = mbal(mover);
     Mask A{};
     if (many(M)) {
       // Bit-sliced equality instead of a loop over trains: for each bit of the cell index, one
@@ -770,7 +845,7 @@ struct WEnv {
 #pragma unroll
       for (int k = 0; k < TPL; ++k) onmap[k] = mine[k] && pos[k] >= 0;
       Mask same[TPL], occs[TPL];
-      const Mask occ0 = mballot<TPL>(onmap);
+      const Mask occ0 = mbal(onmap);
 #pragma unroll
       for (int k = 0; k < TPL; ++k) {
         same[k] = M;
@@ -783,7 +858,7 @@ struct WEnv {
           pd_[k] = mover[k] && (((uint32_t)desired[k] >> bi) & 1u);
           pp_[k] = onmap[k] && (((uint32_t)pos[k] >> bi) & 1u);
         }
-        const Mask bd = mballot<TPL>(pd_), bp = mballot<TPL>(pp_);
+        const Mask bd = mbal(pd_), bp = mbal(pp_);
 #pragma unroll
         for (int k = 0; k < TPL; ++k) {
           const bool one = ((uint32_t)desired[k] >> bi) & 1u;
@@ -795,7 +870,7 @@ struct WEnv {
         bool pn[TPL];
 #pragma unroll
         for (int k = 0; k < TPL; ++k) pn[k] = mover[k] && desired[k] < 0;
-        const Mask bd = mballot<TPL>(pn);
+        const Mask bd = mbal(pn);
 #pragma unroll
         for (int k = 0; k < TPL; ++k) {
           same[k] &= desired[k] < 0 ? bd : ~bd;
@@ -807,7 +882,7 @@ struct WEnv {
       int occ[TPL];
 #pragma unroll
       for (int k = 0; k < TPL; ++k) {
-        const int h = lane + 64 * k;
+        const int h = lane + G * k;
         win[k] = mover[k] && !many(same[k] & mbelow(Mask{}, h));
         const Mask occset = occs[k] & ~mone(Mask{}, h);
         occ[k] = (mover[k] && many(occset)) ? mhighest(occset) : -1;
@@ -816,10 +891,10 @@ struct WEnv {
         bool cand[TPL];
 #pragma unroll
         for (int k = 0; k < TPL; ++k) {
-          const int h = lane + 64 * k;
+          const int h = lane + G * k;
           cand[k] = mover[k] && win[k] && !mbit(A, h) && (occ[k] < 0 || (mbit(M, occ[k]) && mbit(A, occ[k])));
         }
-        const Mask nb = mballot<TPL>(cand);
+        const Mask nb = mbal(cand);
         if (!many(nb)) break;
         A |= nb;
       }
@@ -830,7 +905,7 @@ struct WEnv {
     bool done[TPL], isdone[TPL], newly[TPL], dep[TPL];
 #pragma unroll
     for (int k = 0; k < TPL; ++k) {
-      const int h = lane + 64 * k;
+      const int h = lane + G * k;
       const int32_t t_ed = tt0[k][0], t_target = tt0[k][3], t_init_cell = tt1[k][0];
       const uint32_t t_init_dir = (uint32_t)tt1[k][3] & 0xFFu;
       done[k] = false;
@@ -894,10 +969,10 @@ struct WEnv {
         bits[k] = tb_make(dir, st_, tb_prev(b), saved, mf, done[k] ? 1u : 0u);
       }
     }
-    arr_mask |= mballot<TPL>(newly);
+    arr_mask |= mbal(newly);
     SFL_LAP(13);
     // delete the semaphores of done trains (switch_env.py:370-376): each lane its own records
-    const Mask DONE = mballot<TPL>(done);
+    const Mask DONE = mbal(done);
     if (many(DONE)) {
 #pragma unroll
       for (int k = 0; k < PPL; ++k) {
@@ -906,12 +981,12 @@ struct WEnv {
       }
     }
     // departure semaphores, in handle order (switch_env.py:379-384)
-    Mask D = mballot<TPL>(dep);
+    Mask D = mbal(dep);
     while (many(D)) {
       const int j = mctz(D);
       mclear_low(D);
       const int32_t ed = ltt[8 * j];
-      sset((int)(trl(nprv, j) & 0xFFFFu), r_pack(j, 1, ed - 2, ed + ldc(m.tr_pack, (size_t)j * 8 + 5)));
+      sset((int)(trl(nprv, j) & 0xFFFFu), r_pack(j, 1, ed - 2, ed + LDC(m.tr_pack, (size_t)j * 8 + 5)));
     }
     // pass 4: extend_semaphores (rail_network.py:229-244)
     bool smp[TPL], map_[TPL], mfp[TPL];
@@ -922,7 +997,7 @@ struct WEnv {
       map_[k] = mine[k] && st4 == S_MALF;
       mfp[k] = mine[k] && tb_mf(bits[k]) > 0;
     }
-    const Mask SM = mballot<TPL>(smp);
+    const Mask SM = mbal(smp);
     if (many(SM)) {
 #pragma unroll
       for (int k = 0; k < PPL; ++k) {
@@ -931,15 +1006,15 @@ struct WEnv {
         sem(k) = ext ? r_retime(r, t) : r;
       }
     }
-    Mask MA = mballot<TPL>(map_);
+    Mask MA = mbal(map_);
     while (many(MA)) {
       const int j = mctz(MA);
       mclear_low(MA);
       const int p = (int)(trl(nprv, j) & 0xFFFFu);
-      if (!r_present(sget(p))) sset(p, r_pack(j, 1, t, t + ldc(m.tr_pack, (size_t)j * 8 + 5)));
+      if (!r_present(sget(p))) sset(p, r_pack(j, 1, t, t + LDC(m.tr_pack, (size_t)j * 8 + 5)));
     }
     // malfunction count (switch_env.py:399-401)
-    const Mask MF = mballot<TPL>(mfp);
+    const Mask MF = mbal(mfp);
     n_mf += mpopc(MF & ~mf_mask);
     mf_mask = MF;
     SFL_LAP(14);
@@ -969,10 +1044,10 @@ struct WEnv {
         }
       }
     }
-    q_mask = mballot<TPL>(act);
+    q_mask = mbal(act);
     SFL_LAP(15);
     const Mask full = mfirst(Mask{}, m.T);
-    const Mask ALL = mballot<TPL>(isdone);
+    const Mask ALL = mbal(isdone);
     ep_ticks += 1;
     if ((ALL & full) == full || over) flags |= F_TERM;
   }
@@ -988,21 +1063,41 @@ struct WEnv {
   __device__ __forceinline__ void prefetch(bool greedy) {
     const Mask malf = malf_mask();
 #pragma unroll
+    for (int k = 0; k < TPL; ++k) pf_roff[k] = pf_qoff[k] = PF_NONE;
+    // one train slot at a time (not unrolled): the slots' loads would otherwise be interleaved and
+    // hold twice the registers; the slot's registers are selected by value, not indexed
+#pragma unroll 1
     for (int k = 0; k < TPL; ++k) {
-      pf_roff[k] = pf_qoff[k] = PF_NONE;
-      if (mbit(q_mask, lane + 64 * k)) prefetch_slot(k, malf, greedy);
+      if (!mbit(q_mask, lane + G * k)) continue;
+      uint32_t roff, qoff;
+      prefetch_slot(lane + G * k, pick(sdec, k), pick(nprv, k), pick(bits, k), pick(pos, k), pick(plan, k), malf, greedy,
+                    roff, qoff);
+#pragma unroll
+      for (int j = 0; j < TPL; ++j) {
+        pf_roff[j] = j == k ? roff : pf_roff[j];
+        pf_qoff[j] = j == k ? qoff : pf_qoff[j];
+      }
     }
   }
-  // train slot ks of this lane (train lane + 64 ks) is queued: stage its decision's inputs
-  __device__ __forceinline__ void prefetch_slot(int ks, Mask malf, bool greedy) {
-    const int hk = lane + 64 * ks;
+  template <class T>
+  __device__ __forceinline__ static T pick(const T (&x)[TPL], int k) {
+    T v = x[0];
+#pragma unroll
+    for (int j = 1; j < TPL; ++j) v = j == k ? x[j] : v;
+    return v;
+  }
+  // train hk (one of this lane's slots) is queued: stage its decision's inputs; its registers are
+  // passed by value (sdec, nprv, bits, pos, plan); returns the staged row and pending-cell offsets
+  __device__ __forceinline__ void prefetch_slot(const int hk, const uint32_t sdec_k, const uint32_t nprv_k,
+                                                const uint32_t bits_k, const int32_t pos_k, const uint32_t plan_k, Mask malf,
+                                                bool greedy, uint32_t& roff_out, uint32_t& qoff_out) {
     // Loads are issued by dependency level, unconditionally (clamped indices), so the chains
     // overlap: level 1 needs only this train's registers, level 2 the level-1 results, ...
-    const int sw = (int)(sdec[ks] >> 16);
-    const int pin = (int)(nprv[ks] & 0xFFFFu);
+    const int sw = (int)(sdec_k >> 16);
+    const int pin = (int)(nprv_k & 0xFFFFu);
     const int slot = pin & 3;
-    const int dir0 = (int)tb_dir(bits[ks]);
-    const int pos0 = pos[ks] >= 0 ? pos[ks] : 0;
+    const int dir0 = (int)tb_dir(bits_k);
+    const int pos0 = pos_k >= 0 ? pos_k : 0;
     double* pfl = lpf + PF_W * hk;
     int32_t* pfi = (int32_t*)pfl + PF_I;
     // level 1: slot word, switch record, timetable row, the row block's port record, first moves
@@ -1012,8 +1107,8 @@ struct WEnv {
     const vec_t<uint32_t, 2> nbw = ld((const vec_t<uint32_t, 2>*)m.sw_pack, (size_t)sw * 8u + 4u);
     const vec_t<int32_t, 4> trw = *(const vec_t<int32_t, 4>*)(ltt + 8 * hk);  // ed, la, k, target
     const u4 pr = ld((const u4*)m.port_pack, (size_t)(4 * sw + slot));
-    const uint32_t n_plan = pl_len(plan[ks]);
-    const uint32_t a1 = n_plan ? pl_front(plan[ks]) : A_FWD;
+    const uint32_t n_plan = pl_len(plan_k);
+    const uint32_t a1 = n_plan ? pl_front(plan_k) : A_FWD;
     // move-table rows (all four rail actions) at the cell and after the first rail action
     const u4 row0 = ld((const u4*)m.move_tab, (size_t)((uint32_t)pos0 * 4u + (uint32_t)dir0));
     auto mv_in = [](const u4& r, uint32_t a) -> Move {
@@ -1023,11 +1118,12 @@ struct WEnv {
     // distances the decision needs (reward_func.py:23-78): at the cell, along the STOP plan
     // ([STOP] + plan) and along each route's plan ([front or FWD, final rail action 1..3])
     const int32_t la = (int32_t)trw[1], k = (int32_t)trw[2];
-    const int32_t dd = dist_v(k, pos[ks], dir0);
+    const int32_t dd = dist_v(k, pos_k, dir0);
+    int32_t d_stop, d_rt[4];
     {
-      int pc = pos[ks], pd = dir0;
+      int pc = pos_k, pd = dir0;
       for (uint32_t i = 0; i < n_plan; ++i) {
-        const uint32_t a = pl_at(plan[ks], i);
+        const uint32_t a = pl_at(plan_k, i);
         if (i == 0 && a != A_STOP && pc >= 0) {
           const Move mv = mv_in(row0, a);
           pc = mv.cell;
@@ -1036,17 +1132,17 @@ struct WEnv {
           project(a, pc, pd);
         }
       }
-      pfi[1] = dist_v(k, pc, pd);
+      d_stop = dist_v(k, pc, pd);
     }
     {
-      int pc = pos[ks], pd = dir0;
-      if (a1 != A_STOP && pos[ks] >= 0) {
+      int pc = pos_k, pd = dir0;
+      if (a1 != A_STOP && pos_k >= 0) {
         const Move m1 = mv_in(row0, a1);
         pc = m1.cell;
         pd = m1.dir;
       }
       const u4 row1 = ld((const u4*)m.move_tab, (size_t)((uint32_t)(pc >= 0 ? pc : 0) * 4u + (uint32_t)pd));
-      pfi[2] = 0;  // final rail action 0 (DO_NOTHING) is never a route's
+      d_rt[0] = 0;  // final rail action 0 (DO_NOTHING) is never a route's
 #pragma unroll
       for (uint32_t t = 1; t < 4; ++t) {
         int qc = pc, qd = pd;
@@ -1055,10 +1151,9 @@ struct WEnv {
           qc = mv.cell;
           qd = mv.dir;
         }
-        pfi[2 + t] = dist_v(k, qc, qd);
+        d_rt[t] = dist_v(k, qc, qd);
       }
     }
-    pfi[0] = dd;
     // level 2: the pending update's block; the observation (LDS) and its row
     const uint32_t pend = greedy ? PEND_NONE : slot_pend(slw, epoch);
     const bool hp = pend != PEND_NONE;
@@ -1077,7 +1172,7 @@ struct WEnv {
     const uint32_t lvl = dl <= 0 ? 0u : (dl <= avail * 20 ? 1u : 2u);
     const uint32_t state = ((fb * (uint32_t)m.K) + (uint32_t)k) * 3u + lvl;
     const uint32_t w = pr[1] >> 16, roff = pr[3] + state * w;
-    const bool row_ok = pos[ks] >= 0 && dd < DIST_INF && (pin >> 2) == sw && slot < np;
+    const bool row_ok = pos_k >= 0 && dd < DIST_INF && (pin >> 2) == sw && slot < np;
     const uint32_t qoff = pp[3] + ((pend >> 14) & 0x3FFFu) * (pp[1] >> 16) + ((pend >> 28) & 3u);
     // level 3: Q values
     // (PART: the rows live on their owners; nothing is staged)
@@ -1120,12 +1215,14 @@ struct WEnv {
         amx = b2 ? v : amx;
       }
       pfl[2] = mx;
-      pfi[6] = (best & 0xFF) | ((arg & 0xFF) << 8);
+      pfi[2] = d16(d_rt[3]) | ((uint32_t)((best & 0xFF) | ((arg & 0xFF) << 8)) << 16);
     }
     pfl[0] = qv;
     pfl[1] = __longlong_as_double((long long)slw);
-    pf_roff[ks] = (row_ok && !PART) ? roff : PF_NONE;
-    pf_qoff[ks] = (hp && !PART) ? qoff : PF_NONE;
+    pfi[0] = d16(dd) | (d16(d_stop) << 16);
+    pfi[1] = d16(d_rt[1]) | (d16(d_rt[2]) << 16);
+    roff_out = (row_ok && !PART) ? roff : PF_NONE;
+    qoff_out = (hp && !PART) ? qoff : PF_NONE;
   }
   // a Q cell of this env was written (uniform offset): drop staged copies that contain it
   __device__ __forceinline__ void pf_written(uint32_t off) {
@@ -1176,7 +1273,7 @@ struct WEnv {
     const uint32_t sd = trl(sdec, h);
     const int sw = (int)(sd >> 16);
     const SwRec swr = sw_rec(sw);
-    const vec_t<int32_t, 8> tr = ldcv<vec_t<int32_t, 8>>(m.tr_pack, (size_t)h);
+    const vec_t<int32_t, 8> tr = LDCV<vec_t<int32_t, 8>>(m.tr_pack, (size_t)h);
     const double* pfh = lpf + PF_W * h;
     // the decision's LDS reads that do not depend on its observation, issued together: the staged
     // slot word (never stale: a decision writes only its own train's slots), row column, pending
@@ -1184,10 +1281,8 @@ struct WEnv {
     const uint64_t slot_v = (uint64_t)__double_as_longlong(pfh[1]);
     const double pf_qp = pfh[0];
     const double pf_mx = pfh[2];
-    const vec_t<int32_t, 2> pfd01 = *(const vec_t<int32_t, 2>*)((const int32_t*)pfh + PF_I);
-    const vec_t<int32_t, 2> pfd23 = *(const vec_t<int32_t, 2>*)((const int32_t*)pfh + PF_I + 2);
-    const vec_t<int32_t, 2> pfd45 = *(const vec_t<int32_t, 2>*)((const int32_t*)pfh + PF_I + 4);
-    const vec_t<int32_t, 2> pfd67 = *(const vec_t<int32_t, 2>*)((const int32_t*)pfh + PF_I + 6);
+    const vec_t<uint32_t, 2> pfd01 = *(const vec_t<uint32_t, 2>*)((const uint32_t*)pfh + PF_I);
+    const vec_t<uint32_t, 2> pfd23 = *(const vec_t<uint32_t, 2>*)((const uint32_t*)pfh + PF_I + 2);
     uint64_t rng_w[5];
 #pragma unroll
     for (int i = 0; i < 5; ++i) rng_w[i] = lrng[i];
@@ -1215,12 +1310,12 @@ struct WEnv {
     const Mask malf = malf_mask();
     const uint32_t rn = lsem[nbj], ro = lsem[pj];
     const uint32_t blk = rec_blocks(rn, (uint32_t)h, malf, 0u) | rec_blocks(ro, (uint32_t)h, malf, 1u);
-    const uint32_t free_bits = (uint32_t)__ballot(pvalid && blk == 0u) & 15u;
+    const uint32_t free_bits = (uint32_t)BAL(pvalid && blk == 0u) & 15u;
     SFL_LAP(2);
     const uint32_t b = trl(bits, h);
     const int32_t p0 = trl(pos, h);
     const int32_t ed = tr[0], la = tr[1], k = tr[2];
-    const int32_t d_obs = observe_only ? dist(k, p0, (int)tb_dir(b)) : dist_staged(uni(pfd01[0]));
+    const int32_t d_obs = observe_only ? dist(k, p0, (int)tb_dir(b)) : dist_staged(d16_lo(U(pfd01[0])));
     const int32_t dl = now - la + d_obs;
     const int32_t avail = la - ed;
     const uint32_t lvl = dl <= 0 ? 0u : (dl <= avail * 20 ? 1u : 2u);
@@ -1228,7 +1323,7 @@ struct WEnv {
     const uint32_t la7 = (uint32_t)lane & 7u;
     const uint32_t srca = (swr.w[1] >> (2u * la7)) & 3u, dsta = (swr.w[1] >> (16u + 2u * la7)) & 3u;
     const uint32_t amask =
-        ((uint32_t)__ballot(lane < na - 1 && srca == (uint32_t)slot && ((free_bits >> dsta) & 1u)) & 0xFFu) |
+        ((uint32_t)BAL(lane < na - 1 && srca == (uint32_t)slot && ((free_bits >> dsta) & 1u)) & 0xFFu) |
         (1u << (na - 1));
     SFL_LAP(3);
     SFL_PACC(0, t_obs);
@@ -1248,7 +1343,7 @@ struct WEnv {
       SFL_PCNT(5);
     }
     SFL_LAP(4);
-    d.slotword = uni(slot_v);
+    d.slotword = U(slot_v);
     const uint32_t pend = greedy ? PEND_NONE : slot_pend(d.slotword, epoch);
     d.qoff_pend = PF_NONE;
     double q_pend_v = 0.0;
@@ -1283,12 +1378,12 @@ struct WEnv {
       rng.slo = rng_w[1];
       rng.ihi = rng_w[2];
       rng.ilo = rng_w[3];
-      rng.has = uni((uint32_t)(rng_w[4] >> 32));  // uniform: pcg_next32's branch on it stays scalar
+      rng.has = U((uint32_t)(rng_w[4] >> 32));  // uniform: pcg_next32's branch on it stays scalar
       rng.buf = (uint32_t)rng_w[4];
       const uint32_t n = n_sw;
       // eps0 * decay**n (distr_q.py:59-68): host-computed table (a scalar load, K$-resident), pow beyond it
-      const double eps = n < (uint32_t)m.ntab ? ldc(m.eps_tab, (size_t)n) : m.eps0 * pow_ool(m.eps_decay, (double)n);
-      explore = unid(pcg_double(rng)) < eps;
+      const double eps = n < (uint32_t)m.ntab ? LDC(m.eps_tab, (size_t)n) : m.eps0 * pow_ool(m.eps_decay, (double)n);
+      explore = Ud(pcg_double(rng)) < eps;
       if (explore && !observe_only) {
         const uint32_t sub_seed = pcg_bounded(rng, 2147483646u);
         const uint32_t nvalid = (uint32_t)__builtin_popcount(amask);
@@ -1298,7 +1393,7 @@ struct WEnv {
         uint32_t pick = 0;
         bool slow = nvalid > 1u;
         if (slow && m.seedseq32) {
-          const uint64_t mm = (uint64_t)ldc(m.seedseq32, (size_t)uni(sub_seed)) * nvalid;
+          const uint64_t mm = (uint64_t)LDC(m.seedseq32, (size_t)U(sub_seed)) * nvalid;
           // Lemire rejects when the low word is below (2^32 - n) % n < n: test against n first
           slow = (uint32_t)mm < nvalid && (uint32_t)mm < (0u - nvalid) % nvalid;
           pick = (uint32_t)(mm >> 32);
@@ -1312,7 +1407,7 @@ struct WEnv {
         const uint32_t la16 = (uint32_t)lane & 15u;
         const bool is_pick = lane < 16 && ((amask >> la16) & 1u) &&
                              (uint32_t)__builtin_popcount(amask & ((1u << la16) - 1u)) == pick;
-        action = ctz64(__ballot(is_pick));
+        action = ctz64(BAL(is_pick));
       }
       if (!observe_only) {  // uniform values, written by every lane
         lrng[0] = rng.shi;
@@ -1329,7 +1424,7 @@ struct WEnv {
       flags &= ~F_REQ;
     }
     SFL_LAP(6);
-    d.q_pend = unid(q_pend_v);
+    d.q_pend = Ud(q_pend_v);
     // np.argmax over the full row (first maximum), max(row), and the first allowed maximum
     // (distr_q.py:449-490), over the compact columns held by lanes 0..w-1 (column order = action
     // order, so the lowest lane among equal values is the first index): column c holds full-row
@@ -1338,14 +1433,14 @@ struct WEnv {
     int best, arg;
     if constexpr (PART) {
       // the owner's reply: max over the full row, and the masked argmax (-1 for an exploratory request)
-      const uint32_t ix = uni(ld(P->req_ix, (size_t)e));
+      const uint32_t ix = U(ld(P->req_ix, (size_t)e));
       const vec_t<int32_t, 4> rw =
           ld((const vec_t<int32_t, 4>*)(P->rep_in + (size_t)(ix >> 24) * (P->cap_req + 1) + (ix & 0xFFFFFFu)), 0);
-      best = arg = uni(rw[0]);
-      mx = __longlong_as_double(((long long)(uint32_t)uni(rw[3]) << 32) | (long long)(uint32_t)uni(rw[2]));
+      best = arg = U(rw[0]);
+      mx = __longlong_as_double(((long long)(uint32_t)U(rw[3]) << 32) | (long long)(uint32_t)U(rw[2]));
     } else if (row_hit) {
-      mx = unid(pf_mx);
-      const uint32_t ba = uni((uint32_t)pfd67[0]);
+      mx = Ud(pf_mx);
+      const uint32_t ba = U(pfd23[0]) >> 16;
       best = (int)(ba & 0xFFu);
       arg = (int)((ba >> 8) & 0xFFu);
     } else {
@@ -1356,11 +1451,11 @@ struct WEnv {
       const double vq = colv ? v_c : NEG;
       const double vm = (colv && ((amask >> a_c) & 1u)) ? v_c : NEG;
       const double mq4 = quad_max(vq), am4 = quad_max(vm);
-      const double mqu = unid(mq4), amu = unid(am4);
-      const int cb = ctz64(__ballot(colv && v_c == mqu));
-      const int ca = ctz64(__ballot(vm == amu && colv && ((amask >> a_c) & 1u)));
-      mx = __longlong_as_double(((long long)(uint32_t)__builtin_amdgcn_readlane((int)(__double_as_longlong(v_c) >> 32), cb) << 32) |
-                                (long long)(uint32_t)__builtin_amdgcn_readlane((int)__double_as_longlong(v_c), cb));
+      const double mqu = Ud(mq4), amu = Ud(am4);
+      const int cb = ctz64(BAL(colv && v_c == mqu));
+      const int ca = ctz64(BAL(vm == amu && colv && ((amask >> a_c) & 1u)));
+      mx = __longlong_as_double(((long long)RL((uint32_t)(__double_as_longlong(v_c) >> 32), cb) << 32) |
+                                (long long)RL((uint32_t)__double_as_longlong(v_c), cb));
       best = (int)((rd >> (4 * cb)) & 15u);
       if (mind != 15 && (m.default_q > mx || (m.default_q == mx && mind < best))) {
         mx = m.default_q;
@@ -1374,7 +1469,7 @@ struct WEnv {
     if (!explore) action = ((amask >> best) & 1u) ? best : arg;
     // the exploratory pick comes out of the vector-ALU generator: declare the action wave-uniform,
     // so the apply below branches on the scalar unit instead of through exec-mask regions
-    action = uni(action);
+    action = U(action);
     if (action < 0 || action >= na) lerr |= E_BAD_ACTION;
     SFL_LAP(7);
     SFL_PACC(1, t_eg);
@@ -1397,7 +1492,7 @@ struct WEnv {
     bool blk_moving = false;
     if (moving) {
       // transition_train / transition_semaphore (rail_network.py:246-278, 303-416)
-      const u4 rc = ldcv<u4>(m.port_tr, (size_t)out_p);  // one scalar load for the whole recipe
+      const u4 rc = LDCV<u4>(m.port_tr, (size_t)out_p);  // one scalar load for the whole recipe
       target = (int)(int16_t)(rc[0] & 0xFFFFu);
       if (tb_state(b) != S_MALF) {
         // free the train's records on the ports of its current and previous switch
@@ -1448,7 +1543,7 @@ struct WEnv {
     tset(plan, h, p);
     bool all_blocked;
     if (moving) {
-      all_blocked = uni((uint32_t)blk_moving) != 0u;
+      all_blocked = U((uint32_t)blk_moving) != 0u;
     } else {
       // semaphores unchanged since the observation: no route from the in-port has a free out-port,
       // i.e. the action mask holds STOP only
@@ -1457,8 +1552,9 @@ struct WEnv {
     // reward_func.py:23-78: distance at the position projected along the non-STOP plan (staged
     // by prefetch for the STOP plan and for each final rail action of a route)
     const uint32_t tq = turn & 3u;
-    const int32_t dproj = moving ? (tq == 0 ? pfd23[0] : tq == 1 ? pfd23[1] : tq == 2 ? pfd45[0] : pfd45[1]) : pfd01[1];
-    const int32_t cur = now - la + dist_staged(uni(dproj));
+    const uint32_t dw = U(moving ? (tq == 3 ? pfd23[0] : pfd01[1]) : pfd01[0]);
+    const int32_t dproj = moving ? (tq == 0 ? 0 : tq == 2 ? d16_hi(dw) : d16_lo(dw)) : d16_hi(dw);
+    const int32_t cur = now - la + dist_staged(dproj);
     const int32_t diff = trl(delay, h) - cur;
     d.r_new = (pl_front(p) == A_STOP && !all_blocked) ? diff - 1300 : diff;
     tset(delay, h, cur);
@@ -1585,7 +1681,7 @@ struct WEnv {
     while (many(fresh)) {
       const int tr = mctz(fresh);
       mclear_low(fresh);
-      for (int base = 0; base < m.S; base += 64) {
+      for (int base = 0; base < m.S; base += G) {
         const int sw2 = base + lane;
         const bool valid = sw2 < m.S;
         const uint64_t slw = valid ? ld(slotb, slot_ix(sw2, tr)) : 0ull;
@@ -1639,7 +1735,7 @@ struct WEnv {
     while (many(fresh)) {
       const int tr = mctz(fresh);
       mclear_low(fresh);
-      for (int base = 0; base < m.S; base += 64) {
+      for (int base = 0; base < m.S; base += G) {
         const int sw2 = base + lane;
         const bool valid = sw2 < m.S;
         const uint64_t slw = valid ? ld(slotb, slot_ix(sw2, tr)) : 0ull;
@@ -1661,10 +1757,10 @@ struct WEnv {
     uint64_t c0 = 0;
 #pragma unroll
     for (int k = 0; k < PPL; ++k) {
-      const int p = k * 64 + lane;
+      const int p = k * G + lane;
       if (p < m.NP && r_present(sem(k))) c0 += mix64(((uint64_t)p << 42) ^ r_to64(sem(k)));
     }
-    for (int off = 1; off < 64; off <<= 1) c0 += (uint64_t)__shfl_xor((long long)c0, off, 64);
+    for (int off = 1; off < G; off <<= 1) c0 += (uint64_t)__shfl_xor((long long)c0, off, 64);
     return c0;
   }
 };
@@ -1805,7 +1901,7 @@ __device__ void run(const SflMap& m, const SflState& s, const SflCtl& c, const S
         }
 #pragma unroll
         for (int k = 0; k < V::TPL; ++k)
-          if (v.mine[k]) st(c.st_delays, (row * m.T + lane + 64 * k) * s.E + e, v.delay[k]);
+          if (v.mine[k]) st(c.st_delays, (row * m.T + lane + V::kG * k) * s.E + e, v.delay[k]);
       }
       if (greedy && !test_mode && c.sx_cum && c.stats_cap > 0 && lane == 0) {
         const size_t row = (size_t)(ep_t - c.stats_base) % cap;
@@ -1833,6 +1929,145 @@ __device__ void run(const SflMap& m, const SflState& s, const SflCtl& c, const S
 #endif
   if (lane == 0) {
     if (PART) st(P->dec_done, e, dec_base + (int64_t)v.n_dec);
+    st(s.ep_t, e, ep_t);
+    st(s.n_test, e, n_test);
+    if (c.launch_dec) st(c.launch_dec, e, (uint64_t)v.n_dec);
+    if (c.launch_ticks) st(c.launch_ticks, e, (uint64_t)ticks);
+    if (c.launch_bytes) st(c.launch_bytes, e, (uint64_t)abytes);
+  }
+}
+
+// driver for G < 64 (several envs per wavefront, one per lane group): the same per-env sequence
+// as run() -- decide, post, decide, ..., the last decision of a batch posted after the ticks that
+// follow it -- as a flat loop in which each iteration advances every group by at most one tick,
+// one post step and one decision.  The groups of a wave diverge (one ticks while another decides);
+// a batch loop as in run() would hold every group until the longest batch of the wave is done.
+template <int PPL, int SPL, int TW, bool TRACE, int G>
+__device__ void run_groups(const SflMap& m, const SflState& s, const SflCtl& c) {
+  using V = WEnv<PPL, SPL, TW, false, G>;
+  // per env: semaphores, counters, prefetch records, rng; per block: the timetable rows
+  constexpr int LDS_WORDS = G * (PPL + SPL) + TW * PF_W * 2 + 12;
+  constexpr int EPB = SFL_WAVE_BLOCK / G;  // envs per block (sfl.hip launches)
+  __shared__ uint32_t lds[EPB * LDS_WORDS + TW * 8];
+  const uint32_t e = (uint32_t)((blockIdx.x * blockDim.x + threadIdx.x) / G);
+  if (e >= s.E) return;
+  V v(m, s, e, (int)__lane_id(), lds + (threadIdx.x / G) * LDS_WORDS, nullptr, (int32_t*)(lds + EPB * LDS_WORDS));
+  v.load();
+  int32_t phase = ld(s.phase, e);
+  int32_t ep_t = ld(s.ep_t, e), n_test = ld(s.n_test, e);
+  uint32_t ticks = 0, abytes = 0;
+  typename V::Dec d;
+  d.sw = d.h = d.slot = d.action = d.j = d.reward = d.r_new = d.next_sw = 0;
+  d.state = 0;
+  d.slotword = 0;
+  d.mq = d.q_pend = 0.0;
+  d.qoff_pend = PF_NONE;
+  d.row_pend = 0;
+  d.row_cur = 0;
+  d.touch_cur = false;
+  d.abytes = 0;
+  const bool test_mode = c.mode == 1;
+  const int64_t max_steps = m.max_steps, dec_budget = c.dec_budget;
+  while (true) {
+    if (phase == PH_RESET) {
+      // learn: optional greedy round before episode t (distr_q.py:278-281)
+      bool target = false;
+      if (test_mode) {
+        target = c.ep_target >= 0 && n_test >= c.ep_target;
+        v.flags |= F_GREEDY;
+      } else {
+        target = c.ep_target >= 0 && ep_t >= c.ep_target;
+        if (c.exploit_freq > 0 && (ep_t + 1) % c.exploit_freq == 0 && !(v.flags & F_EXPLOIT_DONE)) v.flags |= F_GREEDY;
+        else v.flags &= ~F_GREEDY;
+      }
+      if (target) break;
+      v.reset();
+      phase = PH_TICK;
+    }
+#ifndef SFL_GROUP_NOSYNC
+    // tick only when no group of the wave can decide: the groups' ticks then run together (a
+    // group that needs a tick waits for the others' batches; measured 14 % faster at G = 16 than
+    // ticking each group as soon as it needs to)
+    const bool wave_decides = __ballot(phase == PH_POST || phase == PH_DECIDE) != 0ull;
+#else
+    const bool wave_decides = false;
+#endif
+    if (phase == PH_TICK && !wave_decides) {
+      abytes += 36u * (uint32_t)(m.T - mpopc(v.arr_mask));
+      v.tick();
+      ticks++;
+      if (v.flags & F_TERM) phase = (v.flags & F_INFLIGHT) ? PH_POST : PH_END;
+      else if (many(v.q_mask)) phase = (v.flags & F_INFLIGHT) ? PH_POST : PH_DECIDE;
+    }
+    if (phase == PH_POST) {  // post step + loop bookkeeping of the decision in flight
+      const bool greedy = (v.flags & F_GREEDY) != 0;
+      v.post(d, greedy);
+      if (TRACE && c.trace && (int32_t)e == c.trace_env) {
+        const uint64_t cs = v.sem_checksum();
+        if (v.lane == 0) {
+          const uint64_t n = *c.trace_n;
+          if (n < (uint64_t)c.trace_cap) {
+            uint64_t* tp = c.trace + 4 * n;
+            tp[0] = (uint64_t)(uint32_t)v.now | ((uint64_t)(uint32_t)d.sw << 16) | ((uint64_t)(uint32_t)d.h << 32) |
+                    ((uint64_t)(uint32_t)d.action << 48);
+            tp[1] = (uint64_t)d.state | ((uint64_t)(uint32_t)d.reward << 32);
+            tp[2] = cs;
+            tp[3] = (uint64_t)(uint32_t)d.next_sw;
+          }
+          *c.trace_n = n + 1;
+        }
+      }
+      v.flags &= ~F_INFLIGHT;
+      v.cum += d.reward;
+      v.ep_dec += 1;
+      v.n_dec += 1;
+      v.step_ctr += 1;
+      if (v.step_ctr > max_steps) v.flags |= F_TRUNC;
+      phase = (v.flags & (F_TERM | F_TRUNC)) ? PH_END : PH_DECIDE;
+      if (dec_budget > 0 && (int64_t)v.n_dec >= dec_budget) break;
+    }
+    if (phase == PH_DECIDE) {
+      const bool greedy = (v.flags & F_GREEDY) != 0;
+      v.decide(d, greedy);
+      abytes += d.abytes;
+      v.flags |= F_INFLIGHT;
+      phase = many(v.q_mask) ? PH_POST : PH_TICK;
+    }
+    if (phase == PH_END) {
+      const int arrived = mpopc(v.arr_mask);
+      const size_t cap = (size_t)(c.stats_cap > 0 ? c.stats_cap : 1);
+      const bool greedy = (v.flags & F_GREEDY) != 0;
+      if (c.st_cum && c.stats_cap > 0 && (!greedy || test_mode)) {
+        const int32_t idx = (greedy && test_mode) ? n_test : ep_t;
+        const size_t row = (size_t)(idx - c.stats_base) % cap;
+        if (v.lane == 0) {
+          st(c.st_cum, row * s.E + e, (double)v.cum);
+          st(c.st_arrived, row * s.E + e, (int32_t)arrived);
+          st(c.st_mf, row * s.E + e, v.n_mf);
+          st(c.st_dec, row * s.E + e, v.ep_dec);
+          st(c.st_ticks, row * s.E + e, v.ep_ticks);
+        }
+#pragma unroll
+        for (int k = 0; k < V::TPL; ++k)
+          if (v.mine[k]) st(c.st_delays, (row * m.T + v.lane + G * k) * s.E + e, v.delay[k]);
+      }
+      if (greedy && !test_mode && c.sx_cum && c.stats_cap > 0 && v.lane == 0) {
+        const size_t row = (size_t)(ep_t - c.stats_base) % cap;
+        st(c.sx_cum, row * s.E + e, (double)v.cum);
+        st(c.sx_arrived, row * s.E + e, (int32_t)arrived);
+      }
+      if (greedy) {
+        if (test_mode) n_test += 1;
+        else v.flags |= F_EXPLOIT_DONE;
+      } else {
+        ep_t += 1;
+        v.flags &= ~F_EXPLOIT_DONE;
+      }
+      phase = PH_RESET;
+    }
+  }
+  v.store(phase);
+  if (v.lane == 0) {
     st(s.ep_t, e, ep_t);
     st(s.n_test, e, n_test);
     if (c.launch_dec) st(c.launch_dec, e, (uint64_t)v.n_dec);

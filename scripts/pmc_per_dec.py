@@ -9,7 +9,10 @@ import sys
 src = sys.argv[1]
 dec = float(sys.argv[2]) if len(sys.argv) > 2 else 65536 * 1024  # bench.py default launch: 65,536 envs x 1024 decisions
 vals = {}
-for f in glob.glob(os.path.join(src, "*counter_collection.csv")) + glob.glob(os.path.join(src, "*", "*counter_collection.csv")):
+files = []
+for d in glob.glob(src):  # a directory, or a glob of several (one per PMC pass)
+    files += glob.glob(os.path.join(d, "*counter_collection.csv")) + glob.glob(os.path.join(d, "*", "*counter_collection.csv"))
+for f in files:
     for r in csv.DictReader(open(f)):
         if "k_run" in r["Kernel_Name"] or "k_wave" in r["Kernel_Name"]:
             vals.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
