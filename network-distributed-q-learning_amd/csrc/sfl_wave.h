@@ -48,15 +48,16 @@ __device__ unsigned long long g_prof[32];
 #endif
 
 constexpr uint32_t PF_NONE = 0xFFFFFFFFu;
-// batch-prefetch record per train (doubles): the pending cell 0, the slot word 1, the staged row's
-// max 2, then int32 words from PF_I: distance-map value at the train's cell (observation), at its
-// projected cell if it stops (reward of STOP), if it moves with final rail action 0..3 (reward of
-// a route), and the row's argmax | first allowed argmax << 8 under the staged observation (the
-// row's columns themselves are not kept: a decision on a staged row needs only its max and argmaxes)
-constexpr int PF_W = 5, PF_I = 6;
-// (the layout, in 32-bit words: 0-1 pending cell value, 2-3 slot word, 4-5 row max; 6: distance at the
-// cell | along the STOP plan << 16, 7: route final action 1 | 2 << 16, 8: route final action 3 |
-// argmax pack << 16 (int16 distances, see d16); 9: spare)
+// batch-prefetch record per train: doubles -- the pending cell, the slot word, the staged row's max;
+// words -- distance-map values at the train's cell (observation), at its projected cell if it stops
+// (reward of STOP), if it moves with final rail action 1..3 (reward of a route), and the row's
+// argmax | first allowed argmax << 8 under the staged observation (the row's columns themselves are
+// not kept: a decision on a staged row needs only its max and argmaxes)
+constexpr int PF_D = 3, PF_WI = 3;  // doubles and 32-bit words of a prefetch record (stored apart: [TW][3] each)
+constexpr int PF_WORDS = 2 * PF_D + PF_WI;
+// (doubles: pending cell value, slot word, row max; words: 0 distance at the cell | along the STOP
+// plan << 16, 1 route final action 1 | 2 << 16, 2 route final action 3 | argmax pack << 16 (int16
+// distances, see d16))
 // distances staged as int16: off the grid -> INT16_MIN, unreachable -> INT16_MAX (choose_variant
 // checks that every finite distance of the map is below 32767)
 __device__ __forceinline__ uint32_t d16(int32_t d) {
@@ -269,7 +270,8 @@ struct WEnv {
   uint32_t* lcnt;  // [64*SPL]
   // batch prefetch (see prefetch()): per queued train (lane), the staged Q row, the pending
   // update's Q cell value and the slot word in LDS, and the staged offsets in VGPRs
-  double* lpf;       // [TW][PF_W]: pending cell value | slot word (as bits) | row max | int32 distances, argmaxes
+  double* lpf;       // [TW][PF_D]: pending cell value | slot word (as bits) | row max
+  uint32_t* lpi;     // [TW][PF_WI]: int16 distances, argmaxes
   uint32_t pf_roff[TPL];  // offset of the staged row in the env's Q block (PF_NONE: none)
   uint32_t pf_qoff[TPL];  // offset of the staged pending cell (PF_NONE: none)
   bool pf_ok;        // uniform: this batch has been prefetched
@@ -307,8 +309,9 @@ struct WEnv {
       mine[k] = lane + G * k < m_.T;
       pf_roff[k] = pf_qoff[k] = PF_NONE;
     }
-    lrng = (uint64_t*)(lds + G * (PPL + SPL) + TWc * PF_W * 2);
-    ltt = ltt_shared ? ltt_shared : (const int32_t*)(lds + G * (PPL + SPL) + TWc * PF_W * 2 + 12);
+    lpi = (uint32_t*)(lpf + TWc * PF_D);
+    lrng = (uint64_t*)(lds + G * (PPL + SPL) + TWc * PF_WORDS);
+    ltt = ltt_shared ? ltt_shared : (const int32_t*)(lds + G * (PPL + SPL) + TWc * PF_WORDS + 12);
     qb = s.q + (size_t)e * m.q_per_env;
     pf_ok = false;
     touchb = s.touched + (size_t)e * m.touched_words;
@@ -325,6 +328,15 @@ struct WEnv {
   __device__ __forceinline__ size_t cix(int sw) const { return (size_t)e * (uint32_t)m.S + (uint32_t)sw; }
 
   // ---- group primitives -------------------------------------------------------------
+  // the lane index in the group, re-read (v_mbcnt) where it is used: values derived from it are then
+  // recomputed inside the loop (one or two VALU) instead of hoisted out of it and spilled -- a
+  // scratch reload is a vector-memory round trip (~600 cycles measured, VmemLatency)
+  __device__ __forceinline__ int lid() const {
+    int x = (int)__lane_id();
+    asm volatile("" : "+v"(x));
+    return G == 64 ? x : (x & (G - 1));
+  }
+  __device__ __forceinline__ bool mine_(int k) const { return lid() + G * k < m.T; }
   // a group-uniform value: in an SGPR for G = 64 (readfirstlane), as is for G < 64
   template <class T>
   __device__ __forceinline__ T U(T x) const {
@@ -374,7 +386,7 @@ struct WEnv {
   __device__ __forceinline__ void sset(int p, uint32_t r) {
     lsem[p] = r;  // wave-uniform value from every lane (one address): no lane-0 exec region
   }
-  __device__ __forceinline__ uint32_t& sem(int k) const { return lsem[k * G + lane]; }  // lane-parallel
+  __device__ __forceinline__ uint32_t& sem(int k) const { return lsem[k * G + lid()]; }  // lane-parallel
   __device__ __forceinline__ uint32_t cget(int sw) const { return U(lcnt[sw]); }
   __device__ __forceinline__ void cset(int sw, uint32_t v) {
     lcnt[sw] = v;  // wave-uniform value from every lane
@@ -395,14 +407,14 @@ struct WEnv {
   template <class T>
   __device__ __forceinline__ void tset(T (&x)[TPL], int h, T v) {
 #pragma unroll
-    for (int k = 0; k < TPL; ++k) x[k] = (lane + G * k == h) ? v : x[k];
+    for (int k = 0; k < TPL; ++k) x[k] = (lid() + G * k == h) ? v : x[k];
   }
   __device__ __forceinline__ uint32_t state_of(int h) const { return tb_state(trl(bits, h)); }
   // malfunctioning trains (check_port_blocked's owner test)
   __device__ __forceinline__ Mask malf_mask() const {
     bool p[TPL];
 #pragma unroll
-    for (int k = 0; k < TPL; ++k) p[k] = mine[k] && tb_state(bits[k]) == S_MALF;
+    for (int k = 0; k < TPL; ++k) p[k] = mine_(k) && tb_state(bits[k]) == S_MALF;
     return mbal(p);
   }
 
@@ -736,6 +748,10 @@ struct WEnv {
   //      flatland_lite.RailEnv.step), train-parallel: lane h = train h ----------------------------
   __device__ __forceinline__ void tick() {
     SFL_LAP0();
+#ifdef SFL_X_NOTICK
+    ++now;
+    return;
+#endif
     pf_ok = false;
     const int32_t t = ++now;
     const uint64_t seed = s.seed[e];
@@ -743,8 +759,8 @@ struct WEnv {
     vec_t<int32_t, 4> tt0[TPL], tt1[TPL];
 #pragma unroll
     for (int k = 0; k < TPL; ++k) {
-      tt0[k] = *(const vec_t<int32_t, 4>*)(ltt + 8 * (mine[k] ? lane + G * k : 0));
-      tt1[k] = *(const vec_t<int32_t, 4>*)(ltt + 8 * (mine[k] ? lane + G * k : 0) + 4);
+      tt0[k] = *(const vec_t<int32_t, 4>*)(ltt + 8 * (mine_(k) ? lid() + G * k : 0));
+      tt1[k] = *(const vec_t<int32_t, 4>*)(ltt + 8 * (mine_(k) ? lid() + G * k : 0) + 4);
     }
     // pass 1: plan pop + prediction, malfunction draw, action preprocessing, desired move
     bool mover[TPL];
@@ -752,14 +768,14 @@ struct WEnv {
     uint32_t aux[TPL];
 #pragma unroll
     for (int k = 0; k < TPL; ++k) {
-      const int h = lane + G * k;
+      const int h = lid() + G * k;
       const int32_t t_init_cell = tt1[k][0];
       const uint32_t t_init_dir = (uint32_t)tt1[k][3] & 0xFFu;
       mover[k] = false;
       desired[k] = -1;
       pred[k] = -1;
       aux[k] = 0;
-      if (mine[k]) {
+      if (mine_(k)) {
         const uint32_t b = bits[k];
         const int32_t p0 = pos[k];
         uint32_t st_ = tb_state(b), dir = tb_dir(b), prev = tb_prev(b), saved = tb_saved(b), mf = tb_mf(b);
@@ -843,7 +859,7 @@ struct WEnv {
       // it (`occs`).  One extra bit keeps an off-grid target (-1) apart from every cell.
       bool onmap[TPL];
 #pragma unroll
-      for (int k = 0; k < TPL; ++k) onmap[k] = mine[k] && pos[k] >= 0;
+      for (int k = 0; k < TPL; ++k) onmap[k] = mine_(k) && pos[k] >= 0;
       Mask same[TPL], occs[TPL];
       const Mask occ0 = mbal(onmap);
 #pragma unroll
@@ -882,7 +898,7 @@ struct WEnv {
       int occ[TPL];
 #pragma unroll
       for (int k = 0; k < TPL; ++k) {
-        const int h = lane + G * k;
+        const int h = lid() + G * k;
         win[k] = mover[k] && !many(same[k] & mbelow(Mask{}, h));
         const Mask occset = occs[k] & ~mone(Mask{}, h);
         occ[k] = (mover[k] && many(occset)) ? mhighest(occset) : -1;
@@ -891,7 +907,7 @@ struct WEnv {
         bool cand[TPL];
 #pragma unroll
         for (int k = 0; k < TPL; ++k) {
-          const int h = lane + G * k;
+          const int h = lid() + G * k;
           cand[k] = mover[k] && win[k] && !mbit(A, h) && (occ[k] < 0 || (mbit(M, occ[k]) && mbit(A, occ[k])));
         }
         const Mask nb = mbal(cand);
@@ -905,14 +921,14 @@ struct WEnv {
     bool done[TPL], isdone[TPL], newly[TPL], dep[TPL];
 #pragma unroll
     for (int k = 0; k < TPL; ++k) {
-      const int h = lane + G * k;
+      const int h = lid() + G * k;
       const int32_t t_ed = tt0[k][0], t_target = tt0[k][3], t_init_cell = tt1[k][0];
       const uint32_t t_init_dir = (uint32_t)tt1[k][3] & 0xFFu;
       done[k] = false;
-      isdone[k] = !mine[k];
+      isdone[k] = !mine_(k);
       newly[k] = false;
       dep[k] = false;
-      if (mine[k]) {
+      if (mine_(k)) {
         const uint32_t b = bits[k];
         const int32_t p0 = pos[k];
         uint32_t st_ = tb_state(b), dir = tb_dir(b), saved = tb_saved(b), mf = tb_mf(b);
@@ -993,9 +1009,9 @@ struct WEnv {
 #pragma unroll
     for (int k = 0; k < TPL; ++k) {
       const uint32_t st4 = tb_state(bits[k]);
-      smp[k] = mine[k] && (st4 == S_STOPPED || st4 == S_MALF);
-      map_[k] = mine[k] && st4 == S_MALF;
-      mfp[k] = mine[k] && tb_mf(bits[k]) > 0;
+      smp[k] = mine_(k) && (st4 == S_STOPPED || st4 == S_MALF);
+      map_[k] = mine_(k) && st4 == S_MALF;
+      mfp[k] = mine_(k) && tb_mf(bits[k]) > 0;
     }
     const Mask SM = mbal(smp);
     if (many(SM)) {
@@ -1024,7 +1040,7 @@ struct WEnv {
     for (int k = 0; k < TPL; ++k) {
       act[k] = false;
       const uint32_t st4 = tb_state(bits[k]);
-      if (mine[k] && pos[k] >= 0 && st4 != S_WAITING) {
+      if (mine_(k) && pos[k] >= 0 && st4 != S_WAITING) {
         const uint32_t nxt = pl_len(plan[k]) ? pl_front(plan[k]) : A_FWD;
         const Move mv = check_action<false>(nxt, pos[k], (int)tb_dir(bits[k]));
         if (mv.cell >= 0) {
@@ -1068,9 +1084,9 @@ struct WEnv {
     // hold twice the registers; the slot's registers are selected by value, not indexed
 #pragma unroll 1
     for (int k = 0; k < TPL; ++k) {
-      if (!mbit(q_mask, lane + G * k)) continue;
+      if (!mbit(q_mask, lid() + G * k)) continue;
       uint32_t roff, qoff;
-      prefetch_slot(lane + G * k, pick(sdec, k), pick(nprv, k), pick(bits, k), pick(pos, k), pick(plan, k), malf, greedy,
+      prefetch_slot(lid() + G * k, pick(sdec, k), pick(nprv, k), pick(bits, k), pick(pos, k), pick(plan, k), malf, greedy,
                     roff, qoff);
 #pragma unroll
       for (int j = 0; j < TPL; ++j) {
@@ -1091,6 +1107,10 @@ struct WEnv {
   __device__ __forceinline__ void prefetch_slot(const int hk, const uint32_t sdec_k, const uint32_t nprv_k,
                                                 const uint32_t bits_k, const int32_t pos_k, const uint32_t plan_k, Mask malf,
                                                 bool greedy, uint32_t& roff_out, uint32_t& qoff_out) {
+#ifdef SFL_X_NOPF
+    roff_out = qoff_out = PF_NONE;
+    return;
+#endif
     // Loads are issued by dependency level, unconditionally (clamped indices), so the chains
     // overlap: level 1 needs only this train's registers, level 2 the level-1 results, ...
     const int sw = (int)(sdec_k >> 16);
@@ -1098,8 +1118,8 @@ struct WEnv {
     const int slot = pin & 3;
     const int dir0 = (int)tb_dir(bits_k);
     const int pos0 = pos_k >= 0 ? pos_k : 0;
-    double* pfl = lpf + PF_W * hk;
-    int32_t* pfi = (int32_t*)pfl + PF_I;
+    double* pfl = lpf + PF_D * hk;
+    uint32_t* pfi = lpi + PF_WI * hk;
     // level 1: slot word, switch record, timetable row, the row block's port record, first moves
     const uint64_t slw = ld(slotb, slot_ix(sw, hk));
     const u4 w0 = ld((const u4*)m.sw_pack, (size_t)sw * 4u);
@@ -1274,18 +1294,21 @@ struct WEnv {
     const int sw = (int)(sd >> 16);
     const SwRec swr = sw_rec(sw);
     const vec_t<int32_t, 8> tr = LDCV<vec_t<int32_t, 8>>(m.tr_pack, (size_t)h);
-    const double* pfh = lpf + PF_W * h;
+    const double* pfh = lpf + PF_D * h;
+    const uint32_t* pfw = lpi + PF_WI * h;
     // the decision's LDS reads that do not depend on its observation, issued together: the staged
     // slot word (never stale: a decision writes only its own train's slots), row column, pending
     // cell value and distances, the epsilon-greedy stream and the switch's interaction count
     const uint64_t slot_v = (uint64_t)__double_as_longlong(pfh[1]);
     const double pf_qp = pfh[0];
     const double pf_mx = pfh[2];
-    const vec_t<uint32_t, 2> pfd01 = *(const vec_t<uint32_t, 2>*)((const uint32_t*)pfh + PF_I);
-    const vec_t<uint32_t, 2> pfd23 = *(const vec_t<uint32_t, 2>*)((const uint32_t*)pfh + PF_I + 2);
+    const uint32_t pfd01[2] = {pfw[0], pfw[1]};
+    const uint32_t pfd23[1] = {pfw[2]};
+#ifndef SFL_X_LATE_RNG
     uint64_t rng_w[5];
 #pragma unroll
     for (int i = 0; i < 5; ++i) rng_w[i] = lrng[i];
+#endif
     const uint32_t n_sw = cget(sw);
     const uint32_t pf_roff_h = trl(pf_roff, h), pf_qoff_h = trl(pf_qoff, h);
     const int np = swr.np();
@@ -1303,9 +1326,9 @@ struct WEnv {
     // switch (observer.py:44-151, 269-283), branch-free integer VALU, then one ballot; lane a
     // evaluates get_action_mask for route a (switch_agents.py:104-134)
     const vec_t<uint32_t, 2> nbw = sw_nb(sw);
-    const int pj = 4 * sw + (lane & 3);
-    const uint32_t nbl = ((lane & 2) ? nbw[1] : nbw[0]) >> ((lane & 1) * 16);
-    const bool pvalid = lane < np;
+    const int pj = 4 * sw + (lid() & 3);
+    const uint32_t nbl = ((lid() & 2) ? nbw[1] : nbw[0]) >> ((lid() & 1) * 16);
+    const bool pvalid = lid() < np;
     const int nbj = pvalid ? (int)(nbl & 0xFFFFu) : pj;
     const Mask malf = malf_mask();
     const uint32_t rn = lsem[nbj], ro = lsem[pj];
@@ -1320,10 +1343,10 @@ struct WEnv {
     const int32_t avail = la - ed;
     const uint32_t lvl = dl <= 0 ? 0u : (dl <= avail * 20 ? 1u : 2u);
     const uint32_t state = ((free_bits * (uint32_t)m.K) + (uint32_t)k) * 3u + lvl;
-    const uint32_t la7 = (uint32_t)lane & 7u;
+    const uint32_t la7 = (uint32_t)lid() & 7u;
     const uint32_t srca = (swr.w[1] >> (2u * la7)) & 3u, dsta = (swr.w[1] >> (16u + 2u * la7)) & 3u;
     const uint32_t amask =
-        ((uint32_t)BAL(lane < na - 1 && srca == (uint32_t)slot && ((free_bits >> dsta) & 1u)) & 0xFFu) |
+        ((uint32_t)BAL(lid() < na - 1 && srca == (uint32_t)slot && ((free_bits >> dsta) & 1u)) & 0xFFu) |
         (1u << (na - 1));
     SFL_LAP(3);
     SFL_PACC(0, t_obs);
@@ -1333,13 +1356,13 @@ struct WEnv {
     const int w = prr.q_w();
     const uint32_t roff = prr.q_off() + state * (uint32_t)w;
     // lane c < w holds compact column c of the row (staged by prefetch unless stale)
-    const bool colv = lane < w;
+    const bool colv = lid() < w;
     const bool row_hit = pf_roff_h == roff;  // the staged row and its greedy choice are valid
     double v_c = 0.0;
     if (row_hit) {
       SFL_PCNT(4);
     } else if (!PART) {
-      v_c = ld(qbase() + roff, (size_t)(colv ? lane : 0));
+      v_c = ld(qbase() + roff, (size_t)(colv ? lid() : 0));
       SFL_PCNT(5);
     }
     SFL_LAP(4);
@@ -1370,10 +1393,19 @@ struct WEnv {
     // epsilon-greedy
     int action = -1;
     bool explore = false;
+#ifdef SFL_X_NORNG
+    if (false) {
+#else
     if (!greedy) {
+#endif
       // (kept in VGPRs: the 128-bit LCG runs on the vector ALU's 64-bit multiply-adds; the scalar
       // unit is the contended one)
       Pcg64 rng;
+#ifdef SFL_X_LATE_RNG
+      uint64_t rng_w[5];
+#pragma unroll
+      for (int i = 0; i < 5; ++i) rng_w[i] = lrng[i];
+#endif
       rng.shi = rng_w[0];
       rng.slo = rng_w[1];
       rng.ihi = rng_w[2];
@@ -1404,8 +1436,8 @@ struct WEnv {
           pick = pcg_bounded(sub, nvalid - 1u);
         }
         // the pick-th allowed action: lane a holds action a, one ballot of its rank among the allowed
-        const uint32_t la16 = (uint32_t)lane & 15u;
-        const bool is_pick = lane < 16 && ((amask >> la16) & 1u) &&
+        const uint32_t la16 = (uint32_t)lid() & 15u;
+        const bool is_pick = lid() < 16 && ((amask >> la16) & 1u) &&
                              (uint32_t)__builtin_popcount(amask & ((1u << la16) - 1u)) == pick;
         action = ctz64(BAL(is_pick));
       }
@@ -1446,7 +1478,7 @@ struct WEnv {
     } else {
       const uint32_t rd = swr.row_desc(slot);
       const int mind = (int)((rd >> 16) & 15u);
-      const uint32_t a_c = (rd >> (4u * ((uint32_t)lane & 3u))) & 15u;
+      const uint32_t a_c = (rd >> (4u * ((uint32_t)lid() & 3u))) & 15u;
       const double NEG = -__builtin_huge_val();
       const double vq = colv ? v_c : NEG;
       const double vm = (colv && ((amask >> a_c) & 1u)) ? v_c : NEG;
@@ -1499,9 +1531,9 @@ struct WEnv {
         const int x1 = pin >> 2;
         const int x2 = pprev != (int)PORT_NONE ? (pprev >> 2) : -1;
         // lanes 0-3: the ports of switch x1, lanes 4-7: those of x2
-        const int xs = lane < 4 ? x1 : x2;
-        const bool act = lane < 8 && xs >= 0;
-        const int pc = act ? 4 * xs + (lane & 3) : 0;
+        const int xs = lid() < 4 ? x1 : x2;
+        const bool act = lid() < 8 && xs >= 0;
+        const int pc = act ? 4 * xs + (lid() & 3) : 0;
         const uint32_t r = lsem[pc];
         if (act && r_present(r) && r_owner(r) == (uint32_t)h) lsem[pc] = 0u;
       }
@@ -1575,7 +1607,7 @@ struct WEnv {
   // ---- graph-partitioned mode: messages to the owners (sfl_part.h records) ---------------------
   // lane 0: the decision's row request (the row's owner answers max(row) and the masked argmax)
   __device__ __forceinline__ void emit_req(int sw, int slot, uint32_t state, uint32_t amask, bool explore) {
-    if (lane != 0) return;
+    if (lid() != 0) return;
     const int dst = ld(P->owner, (size_t)sw);
     const uint32_t k = atomicAdd(P->cnt + dst, 1u);
     if (k >= P->cap_req) {
@@ -1627,7 +1659,7 @@ struct WEnv {
     }
     SFL_LAP0();
     if (greedy) {
-      if (lane == 0) {
+      if (lid() == 0) {
         if (d.touch_cur) touch_row(d.row_cur);
         st(slotb, slot_ix(d.next_sw, d.h), slot_make(PEND_NONE, d.r_new, epoch));
       }
@@ -1653,7 +1685,7 @@ struct WEnv {
     }
     // every global write of the step from one lane-0 region
     // (SFL_AB_*: timing-only tuning builds that drop one class of store, results invalid)
-    if (lane == 0) {
+    if (lid() == 0) {
       if (hp) {
 #ifndef SFL_AB_NO_QST
         st(qbase(), (size_t)d.qoff_pend, nv);
@@ -1682,7 +1714,7 @@ struct WEnv {
       const int tr = mctz(fresh);
       mclear_low(fresh);
       for (int base = 0; base < m.S; base += G) {
-        const int sw2 = base + lane;
+        const int sw2 = base + lid();
         const bool valid = sw2 < m.S;
         const uint64_t slw = valid ? ld(slotb, slot_ix(sw2, tr)) : 0ull;
         const uint32_t pe = valid ? slot_pend(slw, epoch) : PEND_NONE;
@@ -1710,14 +1742,14 @@ struct WEnv {
   // the decision row's key-set insert was done by its owner when it answered a greedy request
   __device__ __forceinline__ void post_part(const Dec& d, bool greedy) {
     if (greedy) {
-      if (lane == 0) st(slotb, slot_ix(d.next_sw, d.h), slot_make(PEND_NONE, d.r_new, epoch));
+      if (lid() == 0) st(slotb, slot_ix(d.next_sw, d.h), slot_make(PEND_NONE, d.r_new, epoch));
       return;
     }
     const uint32_t pend = slot_pend(d.slotword, epoch);
     const bool hp = pend != PEND_NONE;
     const int ps = hp ? (int)(pend & 0xFFFu) : 0;
     const double lr = lr_of(cget(ps));
-    if (lane == 0) {
+    if (lid() == 0) {
       if (hp) {
         const double r = (double)d.reward;
         const double target = d.sw != ps ? r + m.gamma * d.mq : r;
@@ -1736,7 +1768,7 @@ struct WEnv {
       const int tr = mctz(fresh);
       mclear_low(fresh);
       for (int base = 0; base < m.S; base += G) {
-        const int sw2 = base + lane;
+        const int sw2 = base + lid();
         const bool valid = sw2 < m.S;
         const uint64_t slw = valid ? ld(slotb, slot_ix(sw2, tr)) : 0ull;
         const uint32_t pe = valid ? slot_pend(slw, epoch) : PEND_NONE;
@@ -1774,7 +1806,7 @@ struct WEnv {
 template <int PPL, int SPL, int TW, bool TRACE, bool PART = false>
 __device__ void run(const SflMap& m, const SflState& s, const SflCtl& c, const SflPart* P = nullptr) {
   using V = WEnv<PPL, SPL, TW, PART>;
-  constexpr int LDS_WORDS = 64 * (PPL + SPL) + TW * PF_W * 2 + 12 + TW * 8;  // semaphores, counters, prefetch records, rng, timetable
+  constexpr int LDS_WORDS = 64 * (PPL + SPL) + TW * PF_WORDS + 12 + TW * 8;  // semaphores, counters, prefetch records, rng, timetable
   const int lane = (int)__lane_id();
   const uint32_t e = uni((uint32_t)((blockIdx.x * blockDim.x + threadIdx.x) >> 6));
   if (e >= s.E) return;
@@ -1946,7 +1978,7 @@ template <int PPL, int SPL, int TW, bool TRACE, int G>
 __device__ void run_groups(const SflMap& m, const SflState& s, const SflCtl& c) {
   using V = WEnv<PPL, SPL, TW, false, G>;
   // per env: semaphores, counters, prefetch records, rng; per block: the timetable rows
-  constexpr int LDS_WORDS = G * (PPL + SPL) + TW * PF_W * 2 + 12;
+  constexpr int LDS_WORDS = G * (PPL + SPL) + TW * PF_WORDS + 12;
   constexpr int EPB = SFL_WAVE_BLOCK / G;  // envs per block (sfl.hip launches)
   __shared__ uint32_t lds[EPB * LDS_WORDS + TW * 8];
   const uint32_t e = (uint32_t)((blockIdx.x * blockDim.x + threadIdx.x) / G);

@@ -18,4 +18,4 @@ for f in files:
             vals.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
 for k in sorted(vals):
     v = vals[k][1:] if len(vals[k]) > 1 else vals[k]
-    print(f"{k:24s} per-decision {statistics.median(v) / dec:9.1f}")
+    print(f"{k:32s} per-decision {statistics.median(v) / dec:11.2f}   per launch {statistics.median(v):.4g}")
