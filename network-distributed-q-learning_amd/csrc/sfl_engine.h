@@ -92,7 +92,7 @@ constexpr WaveShape kVariants[] = {{0, 0, 0, 64},   {1, 1, 32, 64},  {4, 1, 32, 
                                    {16, 4, 128, 64}, {4, 1, 16, 16},  {16, 4, 32, 16}, {2, 1, 32, 32}, {8, 2, 32, 32}};
 constexpr int kNumVariants = 10;
 #ifndef SFL_DEFAULT_G
-#define SFL_DEFAULT_G 64  // lane group size chosen where a grouped shape fits (SFL_WAVE_G overrides)
+#define SFL_DEFAULT_G 16  // lane group size chosen where a grouped shape fits (SFL_WAVE_G overrides)
 #endif
 
 // Eligibility: trains fit one or two slots per lane (T <= 128), the env fits the variant's

@@ -158,6 +158,16 @@ __device__ __forceinline__ M2 operator~(M2 a) { return M2{{~a.w[0], ~a.w[1]}}; }
 __device__ __forceinline__ M2& operator|=(M2& a, M2 b) { return a = a | b; }
 __device__ __forceinline__ M2& operator&=(M2& a, M2 b) { return a = a & b; }
 __device__ __forceinline__ bool operator==(M2 a, M2 b) { return a.w[0] == b.w[0] && a.w[1] == b.w[1]; }
+// one 32-bit word for up to 32 trains (bit indices >= 32 read as 0)
+__device__ __forceinline__ bool many(uint32_t m) { return m != 0u; }
+__device__ __forceinline__ int mctz(uint32_t m) { return __builtin_ctz(m); }
+__device__ __forceinline__ void mclear_low(uint32_t& m) { m &= m - 1u; }
+__device__ __forceinline__ int mpopc(uint32_t m) { return __builtin_popcount(m); }
+__device__ __forceinline__ bool mbit(uint32_t m, int i) { return (i < 32) & (((m >> (i & 31)) & 1u) != 0u); }
+__device__ __forceinline__ uint32_t mone(uint32_t, int i) { return 1u << i; }
+__device__ __forceinline__ uint32_t mbelow(uint32_t, int i) { return (1u << i) - 1u; }
+__device__ __forceinline__ int mhighest(uint32_t m) { return 31 - __builtin_clz(m); }
+__device__ __forceinline__ uint32_t mfirst(uint32_t, int n) { return n >= 32 ? ~0u : (1u << n) - 1u; }
 __device__ __forceinline__ bool many(uint64_t m) { return m != 0ull; }
 __device__ __forceinline__ bool many(M2 m) { return (m.w[0] | m.w[1]) != 0ull; }
 __device__ __forceinline__ int mctz(uint64_t m) { return ctz64(m); }
@@ -184,10 +194,11 @@ __device__ __forceinline__ uint64_t mfirst(uint64_t, int n) { return n >= 64 ? ~
 __device__ __forceinline__ M2 mfirst(M2, int n) {
   return n >= 128 ? M2{{~0ull, ~0ull}} : n >= 64 ? M2{{~0ull, (n == 64) ? 0ull : (1ull << (n - 64)) - 1ull}} : M2{{(1ull << n) - 1ull, 0ull}};
 }
-// train masks: one 64-bit word for up to 64 trains, two (M2) for up to 128
+// train masks: one 32-bit word for up to 32 trains, one 64-bit word for up to 64, two (M2) for up to 128
 template <int BITS>
 struct MaskOf {
-  using type = typename std::conditional<(BITS <= 64), uint64_t, M2>::type;
+  using type = typename std::conditional<(BITS <= 32), uint32_t,
+                                         typename std::conditional<(BITS <= 64), uint64_t, M2>::type>::type;
 };
 
 // max over each quad of lanes (DPP quad permutes; the result is valid in every lane of the quad)
@@ -252,7 +263,7 @@ struct WEnv {
   static constexpr int TPL = (TWc + G - 1) / G;  // train slots per lane: trains lane, lane + G, ...
   static constexpr int kG = G;
   static_assert(TPL * G <= 128, "at most 128 train slots per env");
-  using Mask = typename MaskOf<TPL * G>::type;
+  using Mask = typename MaskOf<(TWc <= 32 ? 32 : TPL * G)>::type;
   bool mine[TPL];  // lane + G k < T: slot k holds train lane + G k
   // the lane's trains (slot k = train lane + G k)
   int32_t pos[TPL];
@@ -263,6 +274,11 @@ struct WEnv {
   // timetable constants of train `lane` (tr_pack)
   // timetable constants of the lane's train (tr_pack row) live in LDS and are read where used
   const int32_t* ltt;  // [TW][8]
+  // G < 64: the block's LDS copies of the per-switch and per-port map records (sw_pack [S][16],
+  // port_pack and port_tr [4S][4]); G = 64 reads them with scalar loads
+  const uint32_t* tsw = nullptr;
+  const uint32_t* tpp = nullptr;
+  const uint32_t* tpt = nullptr;
   // this env's semaphore records and switch counters in LDS (one region per wave):
   // uniform reads are broadcast ds_reads, writes one lane's ds_write, and the lane-parallel
   // scans read entries k*64 + lane (conflict-free)
@@ -360,11 +376,11 @@ struct WEnv {
   }
   // one ballot per train slot: bit h = train h
   __device__ __forceinline__ Mask mbal(const bool (&p)[TPL]) const {
-    if constexpr (TPL * G <= 64) {
+    if constexpr (TPL * G <= 64 || TWc <= 32) {
       uint64_t r = 0;
 #pragma unroll
       for (int k = 0; k < TPL; ++k) r |= BAL(p[k]) << (G * k);
-      return r;
+      return (Mask)r;  // (32-bit masks: trains < 32 only)
     } else {
       return M2{{BAL(p[0]), BAL(p[1])}};
     }
@@ -419,13 +435,46 @@ struct WEnv {
   }
 
   // ---- map records --------------------------------------------------------------------
-  __device__ __forceinline__ SwRec sw_rec(int sw) const { return SwRec{LDCV<u8>(m.sw_pack, (size_t)sw * 2u)}; }
+  __device__ __forceinline__ SwRec sw_rec(int sw) const {
+    if constexpr (G == 64) return SwRec{LDCV<u8>(m.sw_pack, (size_t)sw * 2u)};
+    else return SwRec{*(const u8*)(tsw + 16 * sw)};
+  }
   // neighbour ports of the switch's ports 0-3 (16 bits each)
   __device__ __forceinline__ vec_t<uint32_t, 2> sw_nb(int sw) const {
-    return LDCV<vec_t<uint32_t, 2>>(m.sw_pack, (size_t)sw * 8u + 4u);
+    if constexpr (G == 64) return LDCV<vec_t<uint32_t, 2>>(m.sw_pack, (size_t)sw * 8u + 4u);
+    else return *(const vec_t<uint32_t, 2>*)(tsw + 16 * sw + 8);
   }
-  __device__ __forceinline__ PortRec port_rec(int p) const { return PortRec{LDCV<u4>(m.port_pack, (size_t)p)}; }
-  __device__ __forceinline__ int port_nb(int p) const { return (int)(int16_t)(LDC(m.port_pack, (size_t)p * 4) & 0xFFFFu); }
+  __device__ __forceinline__ PortRec port_rec(int p) const {
+    if constexpr (G == 64) return PortRec{LDCV<u4>(m.port_pack, (size_t)p)};
+    else return PortRec{*(const u4*)(tpp + 4 * p)};
+  }
+  __device__ __forceinline__ int port_nb(int p) const { return (int)(int16_t)(port_rec(p).w[0] & 0xFFFFu); }
+  __device__ __forceinline__ u4 port_tr_rec(int o) const {
+    if constexpr (G == 64) return LDCV<u4>(m.port_tr, (size_t)o);
+    else return *(const u4*)(tpt + 4 * o);
+  }
+  // lane-parallel (per-lane index) reads of the same records: vector loads for G = 64, LDS else
+  __device__ __forceinline__ u4 sw_v4(int sw, int q) const {
+    if constexpr (G == 64) return ld((const u4*)m.sw_pack, (size_t)sw * 4u + (uint32_t)q);
+    else return *(const u4*)(tsw + 16 * sw + 4 * q);
+  }
+  __device__ __forceinline__ vec_t<uint32_t, 2> sw_nb_v(int sw) const {
+    if constexpr (G == 64) return ld((const vec_t<uint32_t, 2>*)m.sw_pack, (size_t)sw * 8u + 4u);
+    else return *(const vec_t<uint32_t, 2>*)(tsw + 16 * sw + 8);
+  }
+  __device__ __forceinline__ u4 port_v(int p) const {
+    if constexpr (G == 64) return ld((const u4*)m.port_pack, (size_t)p);
+    else return *(const u4*)(tpp + 4 * p);
+  }
+  // timetable row of train h (group-uniform h): scalar loads for G = 64, the LDS rows else
+  __device__ __forceinline__ vec_t<int32_t, 8> tr_row(int h) const {
+    if constexpr (G == 64) return LDCV<vec_t<int32_t, 8>>(m.tr_pack, (size_t)h);
+    else return *(const vec_t<int32_t, 8>*)(ltt + 8 * h);
+  }
+  __device__ __forceinline__ int32_t tr_init_dist(int h) const {
+    if constexpr (G == 64) return LDC(m.tr_pack, (size_t)h * 8 + 5);
+    else return ltt[8 * h + 5];
+  }
   struct Move {
     int cell, dir;
     bool valid, cell_ok;
@@ -629,7 +678,7 @@ struct WEnv {
                  ((uint64_t)ld(s.masks, (size_t)(k * MAXW + 2 * w + 1) * E + e) << 32));
     };
     auto mask = [&](int k) -> Mask {
-      if constexpr (TPL * G <= 64) return word(k, 0);
+      if constexpr (TPL * G <= 64 || TWc <= 32) return (Mask)word(k, 0);
       else return M2{{word(k, 0), word(k, 1)}};
     };
     q_mask = mask(0);
@@ -681,7 +730,7 @@ struct WEnv {
       st(s.err, e, err);
       auto put = [&](int k, const Mask& mk) {
         uint64_t w[2];
-        constexpr int NWD = TPL * G <= 64 ? 1 : 2;
+        constexpr int NWD = (TPL * G <= 64 || TWc <= 32) ? 1 : 2;
         if constexpr (NWD == 1) {
           w[0] = mk;
           w[1] = 0ull;
@@ -1002,7 +1051,7 @@ struct WEnv {
       const int j = mctz(D);
       mclear_low(D);
       const int32_t ed = ltt[8 * j];
-      sset((int)(trl(nprv, j) & 0xFFFFu), r_pack(j, 1, ed - 2, ed + LDC(m.tr_pack, (size_t)j * 8 + 5)));
+      sset((int)(trl(nprv, j) & 0xFFFFu), r_pack(j, 1, ed - 2, ed + tr_init_dist(j)));
     }
     // pass 4: extend_semaphores (rail_network.py:229-244)
     bool smp[TPL], map_[TPL], mfp[TPL];
@@ -1027,7 +1076,7 @@ struct WEnv {
       const int j = mctz(MA);
       mclear_low(MA);
       const int p = (int)(trl(nprv, j) & 0xFFFFu);
-      if (!r_present(sget(p))) sset(p, r_pack(j, 1, t, t + LDC(m.tr_pack, (size_t)j * 8 + 5)));
+      if (!r_present(sget(p))) sset(p, r_pack(j, 1, t, t + tr_init_dist(j)));
     }
     // malfunction count (switch_env.py:399-401)
     const Mask MF = mbal(mfp);
@@ -1122,11 +1171,11 @@ struct WEnv {
     uint32_t* pfi = lpi + PF_WI * hk;
     // level 1: slot word, switch record, timetable row, the row block's port record, first moves
     const uint64_t slw = ld(slotb, slot_ix(sw, hk));
-    const u4 w0 = ld((const u4*)m.sw_pack, (size_t)sw * 4u);
-    const u4 w4 = ld((const u4*)m.sw_pack, (size_t)sw * 4u + 1u);  // compact-row descriptors
-    const vec_t<uint32_t, 2> nbw = ld((const vec_t<uint32_t, 2>*)m.sw_pack, (size_t)sw * 8u + 4u);
+    const u4 w0 = sw_v4(sw, 0);
+    const u4 w4 = sw_v4(sw, 1);  // compact-row descriptors
+    const vec_t<uint32_t, 2> nbw = sw_nb_v(sw);
     const vec_t<int32_t, 4> trw = *(const vec_t<int32_t, 4>*)(ltt + 8 * hk);  // ed, la, k, target
-    const u4 pr = ld((const u4*)m.port_pack, (size_t)(4 * sw + slot));
+    const u4 pr = port_v(4 * sw + slot);
     const uint32_t n_plan = pl_len(plan_k);
     const uint32_t a1 = n_plan ? pl_front(plan_k) : A_FWD;
     // move-table rows (all four rail actions) at the cell and after the first rail action
@@ -1177,7 +1226,7 @@ struct WEnv {
     // level 2: the pending update's block; the observation (LDS) and its row
     const uint32_t pend = greedy ? PEND_NONE : slot_pend(slw, epoch);
     const bool hp = pend != PEND_NONE;
-    const u4 pp = ld((const u4*)m.port_pack, (size_t)(hp ? 4 * (pend & 0xFFFu) + ((pend >> 12) & 3u) : 0u));
+    const u4 pp = port_v(hp ? 4 * (int)(pend & 0xFFFu) + (int)((pend >> 12) & 3u) : 0);
     const int np = (int)(w0[0] & 15u);
     uint32_t fb = 0;
 #pragma unroll
@@ -1293,7 +1342,7 @@ struct WEnv {
     const uint32_t sd = trl(sdec, h);
     const int sw = (int)(sd >> 16);
     const SwRec swr = sw_rec(sw);
-    const vec_t<int32_t, 8> tr = LDCV<vec_t<int32_t, 8>>(m.tr_pack, (size_t)h);
+    const vec_t<int32_t, 8> tr = tr_row(h);
     const double* pfh = lpf + PF_D * h;
     const uint32_t* pfw = lpi + PF_WI * h;
     // the decision's LDS reads that do not depend on its observation, issued together: the staged
@@ -1524,7 +1573,7 @@ struct WEnv {
     bool blk_moving = false;
     if (moving) {
       // transition_train / transition_semaphore (rail_network.py:246-278, 303-416)
-      const u4 rc = LDCV<u4>(m.port_tr, (size_t)out_p);  // one scalar load for the whole recipe
+      const u4 rc = port_tr_rec(out_p);  // one scalar load (LDS read for G < 64) for the whole recipe
       target = (int)(int16_t)(rc[0] & 0xFFFFu);
       if (tb_state(b) != S_MALF) {
         // free the train's records on the ports of its current and previous switch
@@ -1725,7 +1774,7 @@ struct WEnv {
         const uint32_t pstate = (pe >> 14) & 0x3FFFu;
         const int pj = (int)((pe >> 28) & 3u);
         const double lr = lr_of_var(n);
-        const u4 pr = ld((const u4*)m.port_pack, (size_t)(4 * ps + pslot));
+        const u4 pr = port_v(4 * ps + pslot);
         double* qp = qbase() + pr[3] + (size_t)pstate * (pr[1] >> 16) + pj;
         const double a1 = (1.0 - lr) * ld(qp, 0);
         const double b1 = lr * (1000.0 + m.gamma * 0.0);
@@ -1977,13 +2026,26 @@ __device__ void run(const SflMap& m, const SflState& s, const SflCtl& c, const S
 template <int PPL, int SPL, int TW, bool TRACE, int G>
 __device__ void run_groups(const SflMap& m, const SflState& s, const SflCtl& c) {
   using V = WEnv<PPL, SPL, TW, false, G>;
-  // per env: semaphores, counters, prefetch records, rng; per block: the timetable rows
-  constexpr int LDS_WORDS = G * (PPL + SPL) + TW * PF_WORDS + 12;
+  // per env: semaphores, counters, prefetch records, rng; per block: the timetable rows and the
+  // per-switch / per-port map records (the groups of a wave read different switches' records: LDS
+  // reads instead of vector loads)
+  constexpr int LDS_WORDS = (G * (PPL + SPL) + TW * PF_WORDS + 12 + 3) / 4 * 4;
   constexpr int EPB = SFL_WAVE_BLOCK / G;  // envs per block (sfl.hip launches)
-  __shared__ uint32_t lds[EPB * LDS_WORDS + TW * 8];
+  constexpr int SWX = G * SPL, NPX = G * PPL;  // switches / ports the shape holds
+  constexpr int O_TT = EPB * LDS_WORDS, O_SW = O_TT + TW * 8, O_PP = O_SW + SWX * 16, O_PT = O_PP + NPX * 4;
+  __shared__ __attribute__((aligned(16))) uint32_t lds[O_PT + NPX * 4];
+  for (int i = (int)threadIdx.x; i < m.S * 16; i += (int)blockDim.x) lds[O_SW + i] = m.sw_pack[i];
+  for (int i = (int)threadIdx.x; i < m.NP * 4; i += (int)blockDim.x) {
+    lds[O_PP + i] = m.port_pack[i];
+    lds[O_PT + i] = m.port_tr[i];
+  }
+  __syncthreads();
   const uint32_t e = (uint32_t)((blockIdx.x * blockDim.x + threadIdx.x) / G);
   if (e >= s.E) return;
-  V v(m, s, e, (int)__lane_id(), lds + (threadIdx.x / G) * LDS_WORDS, nullptr, (int32_t*)(lds + EPB * LDS_WORDS));
+  V v(m, s, e, (int)__lane_id(), lds + (threadIdx.x / G) * LDS_WORDS, nullptr, (int32_t*)(lds + O_TT));
+  v.tsw = lds + O_SW;
+  v.tpp = lds + O_PP;
+  v.tpt = lds + O_PT;
   v.load();
   int32_t phase = ld(s.phase, e);
   int32_t ep_t = ld(s.ep_t, e), n_test = ld(s.n_test, e);
