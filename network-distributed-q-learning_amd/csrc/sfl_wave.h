@@ -1131,9 +1131,13 @@ struct WEnv {
     for (int k = 0; k < TPL; ++k) pf_roff[k] = pf_qoff[k] = PF_NONE;
     // one train slot at a time (not unrolled): the slots' loads would otherwise be interleaved and
     // hold twice the registers; the slot's registers are selected by value, not indexed
+    // PART: a launch decides one train per env (the round ends at the next request, and the staging
+    // does not survive the launch): stage that train only
+    const int h_first = PART ? mctz(q_mask) : -1;
 #pragma unroll 1
     for (int k = 0; k < TPL; ++k) {
       if (!mbit(q_mask, lid() + G * k)) continue;
+      if (PART && lid() + G * k != h_first) continue;
       uint32_t roff, qoff;
       prefetch_slot(lid() + G * k, pick(sdec, k), pick(nprv, k), pick(bits, k), pick(pos, k), pick(plan, k), malf, greedy,
                     roff, qoff);
