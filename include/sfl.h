@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define SFL_ABI_VERSION 4
+#define SFL_ABI_VERSION 5
 
 typedef struct sfl_handle sfl_handle;
 
@@ -165,7 +165,20 @@ int sfl_part_begin(sfl_handle* h);  /* start a part step: per-env decision count
 int sfl_part_local(sfl_handle* h, int64_t decisions_per_env, const void* replies, void* requests, void* updates,
                    uint64_t* requests_sent);
 int sfl_part_update(sfl_handle* h, const void* updates);
+/* sfl_part_update with the highest update stage of the received segments known to the caller
+ * (the maximum of the senders' sfl_part_counts[2 * world], carried by its count exchange): no
+ * header read; max_stage < 0 = sfl_part_update */
+int sfl_part_update_stages(sfl_handle* h, const void* updates, int32_t max_stage);
 int sfl_part_answer(sfl_handle* h, const void* requests, void* replies);
+/* this rank's record counts of the last sfl_part_local: out[0 .. world) requests and
+ * out[world .. 2 world) update records per destination, out[2 world] the highest update stage
+ * (cap >= 2 * world + 1) */
+int sfl_part_counts(sfl_handle* h, uint32_t* out, int32_t cap);
+/* queue the handle's work on the caller's stream (a hipStream_t, e.g. torch's current stream,
+ * which its RCCL collectives follow); then sfl_part_update / sfl_part_answer return without a
+ * synchronisation and a round synchronises once, in sfl_part_local (its record counts).  null:
+ * the handle's own stream again */
+int sfl_set_stream(sfl_handle* h, void* stream);
 /* owned Q blocks of one env of the job, written into the full per-env layout of sfl_get_q
  * (other entries untouched); owned key-set bits OR-ed into touched */
 int sfl_part_get_q(sfl_handle* h, uint32_t global_env, double* q, uint32_t* touched);

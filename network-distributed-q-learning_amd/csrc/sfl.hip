@@ -82,8 +82,84 @@ __global__ void __launch_bounds__(256) k_part_local(const sfl::SflMap* __restric
   const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e < s->E) sfl::env_run_part<NW>(*m, *s, *c, *P, e);
 }
+// after the wave kernel: pack each env's staged request and update records into the destination
+// segments (a block reserves its range per destination with one global atomic, the envs their
+// places in it with LDS atomics), and add the envs' launch totals into P->sums.  dense: the
+// lane-per-env kernel wrote the segments itself; only the totals.
+__global__ void __launch_bounds__(256) k_part_compact(const sfl::SflPart* __restrict__ P, const sfl::SflState* __restrict__ s,
+                                                      const sfl::SflCtl* __restrict__ c, int dense) {
+  constexpr int MAXU = 32;  // sfl_part_config caps upd_env
+  __shared__ uint32_t lreq[256], lupd[256], breq[256], bupd[256];
+  __shared__ unsigned long long lsum[3];
+  __shared__ uint32_t lerr, lmax;
+  const int world = P->world;
+  for (int i = threadIdx.x; i < world; i += blockDim.x) lreq[i] = lupd[i] = 0u;
+  if (threadIdx.x == 0) {
+    lsum[0] = lsum[1] = lsum[2] = 0ull;
+    lerr = lmax = 0u;
+  }
+  __syncthreads();
+  const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool valid = e < s->E;
+  int rd = -1;
+  uint32_t kr = 0, nu = 0, ku[MAXU];
+  uint8_t du[MAXU];
+  if (valid) {
+    if (!dense) {
+      rd = P->req_dst[e];
+      if (rd >= 0) kr = atomicAdd(&lreq[rd], 1u);
+      nu = P->upd_n[e];
+      for (uint32_t i = 0; i < nu && i < (uint32_t)MAXU; ++i) {
+        const sfl::PartUpd& u = P->upd_st[(size_t)e * P->upd_env + i];
+        const int d = P->owner[u.port >> 2];
+        du[i] = (uint8_t)d;
+        ku[i] = atomicAdd(&lupd[d], 1u);
+        atomicMax(&lmax, (uint32_t)u.stage);
+      }
+    }
+    atomicAdd(&lsum[0], (unsigned long long)c->launch_dec[e]);
+    atomicAdd(&lsum[1], (unsigned long long)c->launch_ticks[e]);
+    atomicAdd(&lsum[2], (unsigned long long)c->launch_bytes[e]);
+    atomicOr(&lerr, s->err[e]);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < world; i += blockDim.x) {
+    breq[i] = lreq[i] ? atomicAdd(P->cnt + i, lreq[i]) : 0u;
+    bupd[i] = lupd[i] ? atomicAdd(P->cnt + world + i, lupd[i]) : 0u;
+  }
+  if (threadIdx.x == 0) {
+    atomicAdd((unsigned long long*)&P->sums[0], lsum[0]);
+    atomicAdd((unsigned long long*)&P->sums[1], lsum[1]);
+    atomicAdd((unsigned long long*)&P->sums[2], lsum[2]);
+    if (lerr) atomicOr((unsigned long long*)&P->sums[3], (unsigned long long)lerr);
+    if (lmax) atomicMax(P->max_stage, lmax);
+  }
+  __syncthreads();
+  if (!valid || dense) return;
+  uint32_t ovf = 0;
+  if (rd >= 0) {
+    const uint32_t k = breq[rd] + kr;
+    if (k < P->cap_req) {
+      P->req_out[(size_t)rd * (P->cap_req + 1) + 1 + k] = P->req_st[e];
+      P->req_ix[e] = ((uint32_t)rd << 24) | (1u + k);
+    } else {
+      ovf = sfl::E_MSG_OVF;
+    }
+  }
+  for (uint32_t i = 0; i < nu && i < (uint32_t)MAXU; ++i) {
+    const uint32_t d = du[i], k = bupd[d] + ku[i];
+    if (k < P->cap_upd) P->upd_out[(size_t)d * (P->cap_upd + 1) + 1 + k] = P->upd_st[(size_t)e * P->upd_env + i];
+    else ovf = sfl::E_MSG_OVF;
+  }
+  if (ovf) {
+    s->err[e] |= ovf;
+    atomicOr((unsigned long long*)&P->sums[3], (unsigned long long)ovf);
+  }
+}
 __global__ void k_part_headers(const sfl::SflPart* __restrict__ P) {
   if ((int)threadIdx.x < P->world) sfl::part_headers(*P, (int)threadIdx.x);
+  __syncthreads();
+  if (threadIdx.x == 0) sfl::part_finish(*P);
 }
 __global__ void k_part_answer(const sfl::SflMap* __restrict__ m, const sfl::SflPart* __restrict__ P,
                               const sfl::PartReq* __restrict__ in, sfl::PartRep* __restrict__ out) {
@@ -176,7 +252,8 @@ __global__ void k_qinit(sfl::SflMap m, sfl::SflState s, uint32_t n_rows, const u
 
 struct HipBackend {
   static constexpr bool kHasWave = true;
-  hipStream_t stream = nullptr;
+  hipStream_t stream = nullptr;      // the stream every call of the handle queues on
+  hipStream_t own_stream = nullptr;  // the handle's own (stream unless sfl_set_stream chose the caller's)
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   void* d_params = nullptr;  // device copies of SflMap | SflState | SflCtl
   std::string err;
@@ -202,7 +279,8 @@ struct HipBackend {
       return -1;
     }
     if (!check(hipSetDevice(device), "hipSetDevice")) return -1;
-    if (!check(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking), "hipStreamCreate")) return -1;
+    if (!check(hipStreamCreateWithFlags(&own_stream, hipStreamNonBlocking), "hipStreamCreate")) return -1;
+    stream = own_stream;
     if (!check(hipEventCreate(&ev0), "hipEventCreate") || !check(hipEventCreate(&ev1), "hipEventCreate")) return -1;
     if (!check(hipMalloc(&d_params, 4096), "hipMalloc params")) return -1;
     return 0;
@@ -212,7 +290,14 @@ struct HipBackend {
     if (ev1) hipEventDestroy(ev1);
     if (d_params) hipFree(d_params);
     if (d_pparams) hipFree(d_pparams);
-    if (stream) hipStreamDestroy(stream);
+    if (own_stream) hipStreamDestroy(own_stream);
+  }
+  // queue on the caller's stream (e.g. torch's current stream, which its RCCL collectives follow);
+  // null: back to the handle's own
+  int set_stream(void* st) {
+    if (!check(hipStreamSynchronize(stream), "sync")) return -1;
+    stream = st ? (hipStream_t)st : own_stream;
+    return 0;
   }
   void* alloc(size_t bytes) {
     void* p = nullptr;
@@ -410,6 +495,7 @@ struct HipBackend {
     else if (m.T <= 64) k_part_local<2><<<blocks, 64, 0, stream>>>(&pp->m, &pp->s, &pp->c, &pp->P);
     else k_part_local<4><<<blocks, 64, 0, stream>>>(&pp->m, &pp->s, &pp->c, &pp->P);
     if (!check(hipGetLastError(), "k_part_local")) return -1;
+    k_part_compact<<<(s.E + 255) / 256, 256, 0, stream>>>(&pp->P, &pp->s, &pp->c, variant > 0 ? 0 : 1);
     k_part_headers<<<1, 256, 0, stream>>>(&pp->P);
     check(hipEventRecord(ev1, stream), "event");
     // (no synchronisation here: the caller issues the launch totals and the count copies behind

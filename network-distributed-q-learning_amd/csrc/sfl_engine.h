@@ -39,6 +39,9 @@ struct Handle {
   uint64_t last_dec = 0, last_ticks = 0, last_bytes = 0, total_dec = 0;
   uint32_t last_err = 0;
   uint64_t* d_sums = nullptr;  // [4]
+  bool ext_stream = false;     // the caller's stream (sfl_set_stream): owner steps queue without a sync
+  uint32_t part_max_stage = 0;            // of the last part_local
+  std::vector<uint32_t> part_counts;      // of the last part_local: [2 * world + 1]
   uint64_t* d_launch_dec = nullptr;
   uint64_t* d_launch_ticks = nullptr;
   uint64_t* d_launch_bytes = nullptr;
@@ -597,6 +600,10 @@ int part_config(Handle<B>* h, int rank, int world, const int32_t* owner, uint32_
   if (env_base + h->E > E_tot) return fail("sfl_part_config: env range outside envs_total");
   if (cap_req < h->E) return fail("sfl_part_config: request capacity must hold one request per local env");
   if (cap_req >= (1u << 24) || cap_upd < 1) return fail("sfl_part_config: bad capacities");
+  // the wave kernel stages up to upd_env update records per env and round (E_MSG_OVF beyond); the
+  // segments must hold every env's staged records
+  const uint32_t upd_env = cap_upd / h->E < 32u ? cap_upd / h->E : 32u;
+  if (upd_env < 2) return fail("sfl_part_config: update capacity must allow two records per local env");
   const int S = h->map.S, K = h->map.K;
   std::vector<int32_t> own(owner, owner + S);
   for (int s = 0; s < S; ++s)
@@ -642,9 +649,19 @@ int part_config(Handle<B>* h, int rank, int world, const int32_t* owner, uint32_
   P.req_ix = h->template dalloc<uint32_t>(h->E);
   P.dec_done = h->template dalloc<int64_t>(h->E);
   P.cnt = h->template dalloc<uint32_t>(2 * (size_t)world + 1);
-  if (!P.owner || !P.q_own || !P.touched_own || !P.obs || !P.req_ix || !P.dec_done || !P.cnt)
+  P.sums = h->d_sums;
+  P.cnt_out = h->template dalloc<uint64_t>(4 + (size_t)world + 1);
+  P.upd_env = upd_env;
+  P.req_st = h->template dalloc<PartReq>(h->E);
+  P.req_dst = h->template dalloc<int32_t>(h->E);
+  P.upd_st = h->template dalloc<PartUpd>((size_t)h->E * upd_env);
+  P.upd_n = h->template dalloc<uint32_t>(h->E);
+  if (!P.owner || !P.q_own || !P.touched_own || !P.obs || !P.req_ix || !P.dec_done || !P.cnt || !P.cnt_out || !P.req_st ||
+      !P.req_dst || !P.upd_st || !P.upd_n)
     return fail("sfl_part_config: allocation failed (out of memory?)");
   P.max_stage = P.cnt + 2 * world;
+  h->be.memset(P.cnt, 0, (2 * (size_t)world + 1) * 4);
+  h->be.memset(P.sums, 0, 4 * 8);
   h->be.fill_f64(P.q_own, h->map.default_q, (size_t)E_tot * off);
   h->be.memset(P.touched_own, 0, (size_t)E_tot * P.own_words * 4);
   h->be.memset(P.dec_done, 0, h->E * 8);
@@ -741,7 +758,9 @@ int part_begin(Handle<B>* h) {
 }
 
 // local step of a round: every env applies its reply, runs to its next decision and emits the
-// request (and the update records of its post step)
+// request (and the update records of its post step).  One host synchronisation: the record
+// counts and the launch totals, copied behind the kernels (k_part_headers zeroes them for the
+// next round).
 template <class B>
 int part_local(Handle<B>* h, int64_t budget, const void* rep_in, void* req_out, void* upd_out, uint64_t* n_req) {
   SflPart& P = h->part;
@@ -749,7 +768,6 @@ int part_local(Handle<B>* h, int64_t budget, const void* rep_in, void* req_out, 
   P.rep_in = (const PartRep*)rep_in;
   P.req_out = (PartReq*)req_out;
   P.upd_out = (PartUpd*)upd_out;
-  h->be.memset(P.cnt, 0, (2 * (size_t)P.world + 1) * 4);
   SflCtl c{};
   c.mode = 0;
   c.ep_target = -1;
@@ -759,26 +777,33 @@ int part_local(Handle<B>* h, int64_t budget, const void* rep_in, void* req_out, 
   c.launch_bytes = h->d_launch_bytes;
   float ms = 0.f;
   int rc = h->be.part_local(h->map, h->st, c, P, h->variant, &ms);
-  // the launch totals, the record counts and the totals' copy queued behind the kernels: one sync
-  std::vector<uint32_t> cnt(2 * (size_t)P.world + 1);
-  uint64_t sums[4] = {0, 0, 0, 0};
+  std::vector<uint64_t> out(4 + (size_t)P.world + 1);
   if (!rc) {
-    h->be.reduce_launch(h->d_launch_dec, h->d_launch_ticks, h->d_launch_bytes, h->st.err, h->E, h->d_sums);
-    h->be.d2h_async(cnt.data(), P.cnt, cnt.size() * 4);
-    h->be.d2h_async(sums, h->d_sums, sizeof sums);
+    h->be.d2h_async(out.data(), P.cnt_out, out.size() * 8);
     rc = h->be.sync();
   }
   if (rc) return fail(std::string("sfl_part_local: ") + h->be.error());
   h->last_kernel_ms = h->be.elapsed_ms();
-  h->last_dec = sums[0];
-  h->last_ticks = sums[1];
-  h->last_bytes = sums[2];
-  h->last_err = (uint32_t)sums[3];
-  h->total_dec += sums[0];
+  h->last_dec = out[0];
+  h->last_ticks = out[1];
+  h->last_bytes = out[2];
+  h->last_err = (uint32_t)out[3];
+  h->total_dec += out[0];
+  const uint32_t* cnt = (const uint32_t*)(out.data() + 4);
   uint64_t n = 0;
   for (int g = 0; g < P.world; ++g) n += cnt[g];
+  h->part_max_stage = cnt[2 * P.world];
+  h->part_counts.assign(cnt, cnt + 2 * P.world + 1);
   if (n_req) *n_req = n;
   return scan_errors(h);
+}
+
+// the owner steps are queued without a synchronisation when the caller's stream carries the
+// round (sfl_set_stream): launch errors still surface, kernel faults at the next part_local
+template <class B>
+int part_done(Handle<B>* h, const char* what) {
+  if (h->ext_stream) return h->be.error()[0] ? fail(std::string(what) + ": " + h->be.error()) : 0;
+  return h->be.sync() ? fail(std::string(what) + ": " + h->be.error()) : 0;
 }
 
 template <class B>
@@ -786,22 +811,42 @@ int part_answer(Handle<B>* h, const void* req_in, void* rep_out) {
   SflPart& P = h->part;
   if (!P.world) return fail("sfl_part_answer: handle not partitioned");
   h->be.part_answer(h->map, P, (const PartReq*)req_in, (PartRep*)rep_out);
-  return h->be.sync() ? fail(std::string("sfl_part_answer: ") + h->be.error()) : 0;
+  return part_done(h, "sfl_part_answer");
 }
 
+// max_stage: the highest update stage in the received segments (every sender's part_local
+// count, carried by the caller's count exchange); < 0: read it from the segment headers (one
+// more synchronisation); one rank: this rank's own part_local count
 template <class B>
-int part_update(Handle<B>* h, const void* upd_in) {
+int part_update(Handle<B>* h, const void* upd_in, int32_t max_stage = -1) {
   SflPart& P = h->part;
   if (!P.world) return fail("sfl_part_update: handle not partitioned");
   const PartUpd* in = (const PartUpd*)upd_in;
-  uint32_t max_stage = 0;
-  std::vector<PartUpd> hd(P.world);
-  for (int g = 0; g < P.world; ++g) h->be.d2h_async(&hd[g], in + (size_t)g * (P.cap_upd + 1), sizeof(PartUpd));
-  if (h->be.sync()) return fail(h->be.error());
-  for (int g = 0; g < P.world; ++g)
-    if (hd[g].genv > 0 && hd[g].state > max_stage) max_stage = hd[g].state;
-  for (uint32_t st = 0; st <= max_stage; ++st) h->be.part_update(h->map, P, in, (int)st);
-  return h->be.sync() ? fail(std::string("sfl_part_update: ") + h->be.error()) : 0;
+  uint32_t ms = 0;
+  if (max_stage >= 0) {
+    ms = (uint32_t)max_stage;
+  } else if (P.world == 1) {
+    ms = h->part_max_stage;
+  } else {
+    std::vector<PartUpd> hd(P.world);
+    for (int g = 0; g < P.world; ++g) h->be.d2h_async(&hd[g], in + (size_t)g * (P.cap_upd + 1), sizeof(PartUpd));
+    if (h->be.sync()) return fail(h->be.error());
+    for (int g = 0; g < P.world; ++g)
+      if (hd[g].genv > 0 && hd[g].state > ms) ms = hd[g].state;
+  }
+  for (uint32_t st = 0; st <= ms; ++st) h->be.part_update(h->map, P, in, (int)st);
+  return part_done(h, "sfl_part_update");
+}
+
+// this rank's record counts of the last part_local: [2 * world + 1] = requests per destination,
+// updates per destination, highest update stage
+template <class B>
+int part_counts(Handle<B>* h, uint32_t* out, int32_t cap) {
+  if (!h->part.world) return fail("sfl_part_counts: handle not partitioned");
+  const int32_t n = 2 * h->part.world + 1;
+  if (cap < n) return fail("sfl_part_counts: buffer too small");
+  for (int32_t i = 0; i < n; ++i) out[i] = i < (int32_t)h->part_counts.size() ? h->part_counts[i] : 0u;
+  return 0;
 }
 
 }  // namespace sfl

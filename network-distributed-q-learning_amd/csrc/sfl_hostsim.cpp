@@ -81,9 +81,14 @@ struct HostBackend {
       else sfl::env_run_part<4>(m, s, c, P, (uint32_t)e);
     }
     for (int g = 0; g < P.world; ++g) sfl::part_headers(P, g);
+    uint64_t t[4];
+    reduce_launch(c.launch_dec, c.launch_ticks, c.launch_bytes, s.err, s.E, t);
+    for (int i = 0; i < 4; ++i) P.sums[i] = t[i];
+    sfl::part_finish(P);
     *ms = 0.f;
     return 0;
   }
+  int set_stream(void*) { return 0; }  // one host thread: nothing to order
   void part_answer(const sfl::SflMap& m, const sfl::SflPart& P, const sfl::PartReq* in, sfl::PartRep* out) {
     for (int g = 0; g < P.world; ++g) {
       const size_t base = (size_t)g * (P.cap_req + 1);

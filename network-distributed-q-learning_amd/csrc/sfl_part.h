@@ -67,6 +67,16 @@ struct SflPart {
   int64_t* dec_done;          // [E] decisions since sfl_part_begin
   uint32_t* cnt;              // [2][world] records emitted this round (requests, updates)
   uint32_t* max_stage;        // [1] highest update stage emitted this round
+  uint64_t* sums;             // [4] this round's launch totals (decisions, ticks, bytes, error bits OR)
+  uint64_t* cnt_out;          // [4 + world + 1]: sums, then the [2 * world + 1] counts (incl. max_stage) as
+                              // u32: the one host read of a round (part_finish zeroes cnt / sums for the next)
+  // the wave kernel's per-env staging of a round's messages (k_part_compact packs them into the
+  // segments): no record index is taken with a contended atomic counter in the env kernel
+  PartReq* req_st;            // [E] the env's request of this round
+  int32_t* req_dst;           // [E] its destination rank, -1: no request
+  PartUpd* upd_st;            // [E][upd_env] the env's update records of this round
+  uint32_t* upd_n;            // [E] how many
+  uint32_t upd_env;           // staged update records per env and round (E_MSG_OVF beyond)
   // round buffers (set per call)
   const PartRep* rep_in;      // [world][cap_req + 1]
   PartReq* req_out;           // [world][cap_req + 1]
@@ -310,6 +320,20 @@ SFL_FN void part_headers(const SflPart& P, int dst) {
   P.req_out[(size_t)dst * (P.cap_req + 1)].genv = nr < P.cap_req ? nr : P.cap_req;
   P.upd_out[(size_t)dst * (P.cap_upd + 1)].genv = nu < P.cap_upd ? nu : P.cap_upd;
   P.upd_out[(size_t)dst * (P.cap_upd + 1)].state = *P.max_stage;
+}
+
+// after every destination's header: hand the counts and launch totals to the host copy and
+// zero them for the next round (so a round needs no separate clearing step)
+SFL_FN void part_finish(const SflPart& P) {
+  uint32_t* c = (uint32_t*)(P.cnt_out + 4);
+  for (int i = 0; i < 2 * P.world + 1; ++i) {
+    c[i] = P.cnt[i];
+    P.cnt[i] = 0u;
+  }
+  for (int i = 0; i < 4; ++i) {
+    P.cnt_out[i] = P.sums[i];
+    P.sums[i] = 0ull;
+  }
 }
 
 }  // namespace sfl

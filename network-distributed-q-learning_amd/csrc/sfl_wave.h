@@ -308,6 +308,9 @@ struct WEnv {
   int32_t n_mf, ep_dec, ep_ticks;
   int32_t step_ctr;
   uint32_t n_dec;  // decisions in this launch (dec_total += n_dec on store)
+  // PART: this launch's messages, staged in the env's own slots (k_part_compact packs them)
+  int32_t req_dst_v = -1;  // destination of the request (-1: none)
+  uint32_t n_upd = 0;      // update records staged
 #ifdef SFL_PROFILE
   uint64_t prof[9] = {};  // decide: observe, epsilon-greedy, apply; events: prefetch, row hit/miss, pend hit/miss, decisions
   uint64_t lap[16] = {};  // finer segments (see SFL_LAP call sites)
@@ -1658,31 +1661,25 @@ struct WEnv {
   }
 
   // ---- graph-partitioned mode: messages to the owners (sfl_part.h records) ---------------------
-  // lane 0: the decision's row request (the row's owner answers max(row) and the masked argmax)
+  // the decision's row request (the row's owner answers max(row) and the masked argmax), staged in
+  // the env's request slot; k_part_compact gives it its place in the destination segment
   __device__ __forceinline__ void emit_req(int sw, int slot, uint32_t state, uint32_t amask, bool explore) {
+    req_dst_v = U(ld(P->owner, (size_t)sw));
     if (lid() != 0) return;
-    const int dst = ld(P->owner, (size_t)sw);
-    const uint32_t k = atomicAdd(P->cnt + dst, 1u);
-    if (k >= P->cap_req) {
-      lerr |= E_MSG_OVF;
-      return;
-    }
     u4 r;
     r[0] = P->env_base + e;
     r[1] = (uint32_t)(4 * sw + slot) | (amask << 16);
     r[2] = state;
     r[3] = explore ? 1u : 0u;
     static_assert(sizeof(PartReq) == sizeof(u4), "request record");
-    st((u4*)P->req_out, (size_t)dst * (P->cap_req + 1) + 1 + k, r);
-    st(P->req_ix, (size_t)e, ((uint32_t)dst << 24) | (1u + k));
+    st((u4*)P->req_st, (size_t)e, r);
   }
-  // any lane: one update record (kind 0: q <- (1 - lr) q + lr target, and the key-set insert;
-  // kind 1: the key-set insert only) to the owner of switch sw, applied in stage order
-  __device__ __forceinline__ void emit_upd(int sw, int slot, uint32_t state, int j, uint32_t kind, double lr, double target,
-                                           int stage) {
-    const int dst = ld(P->owner, (size_t)sw);
-    const uint32_t k = atomicAdd(P->cnt + P->world + dst, 1u);
-    if (k >= P->cap_upd) {
+  // one update record (kind 0: q <- (1 - lr) q + lr target, and the key-set insert; kind 1: the
+  // key-set insert only) to the owner of switch sw, applied in stage order, staged in slot k of the
+  // env's update slots (k from the wave-uniform count n_upd)
+  __device__ __forceinline__ void emit_upd(uint32_t k, int sw, int slot, uint32_t state, int j, uint32_t kind, double lr,
+                                           double target, int stage) {
+    if (k >= P->upd_env) {
       lerr |= E_MSG_OVF;
       return;
     }
@@ -1696,10 +1693,9 @@ struct WEnv {
     b[2] = (uint32_t)__double_as_longlong(target);
     b[3] = (uint32_t)(__double_as_longlong(target) >> 32);
     static_assert(sizeof(PartUpd) == 2 * sizeof(u4), "update record");
-    u4* u = (u4*)(P->upd_out + (size_t)dst * (P->cap_upd + 1) + 1 + k);
+    u4* u = (u4*)(P->upd_st + (size_t)e * P->upd_env + k);
     st(u, 0, a);
     st(u, 1, b);
-    if (stage > 0) atomicMax(P->max_stage, (uint32_t)stage);
   }
 
   // ---- post-step part of the learn loop (distr_q.py:322-362) -----------------------------------
@@ -1802,12 +1798,16 @@ struct WEnv {
     const bool hp = pend != PEND_NONE;
     const int ps = hp ? (int)(pend & 0xFFFu) : 0;
     const double lr = lr_of(cget(ps));
+    // record slots taken outside the lane-0 region, so the count stays wave-uniform
+    const uint32_t k0 = n_upd;
+    const bool touch_sep = hp && d.sw != ps && !d.touch_cur;
+    n_upd += (hp ? 1u : 0u) + (touch_sep ? 1u : 0u);
     if (lid() == 0) {
       if (hp) {
         const double r = (double)d.reward;
         const double target = d.sw != ps ? r + m.gamma * d.mq : r;
-        emit_upd(ps, (int)((pend >> 12) & 3u), (pend >> 14) & 0x3FFFu, (int)((pend >> 28) & 3u), 0u, lr, target, 0);
-        if (d.sw != ps && !d.touch_cur) emit_upd(d.sw, d.slot, d.state, 0, 1u, 0.0, 0.0, 0);
+        emit_upd(k0, ps, (int)((pend >> 12) & 3u), (pend >> 14) & 0x3FFFu, (int)((pend >> 28) & 3u), 0u, lr, target, 0);
+        if (touch_sep) emit_upd(k0 + 1u, d.sw, d.slot, d.state, 0, 1u, 0.0, 0.0, 0);
       }
       st(slotb, slot_ix(d.sw, d.h), slot_make(PEND_NONE, slot_rew(d.slotword, epoch), epoch));
       st(slotb, slot_ix(d.next_sw, d.h),
@@ -1827,8 +1827,12 @@ struct WEnv {
         const uint32_t pe = valid ? slot_pend(slw, epoch) : PEND_NONE;
         const int ps2 = pe == PEND_NONE ? 0 : (int)(pe & 0xFFFu);
         const uint32_t n = cget_var(ps2);  // all lanes active: a bpermute reads 0 from inactive lanes
+        // this pass's records: slots in lane order after the ones taken so far
+        const uint64_t bm = (uint64_t)BAL(pe != PEND_NONE);
+        const uint32_t k = n_upd + (uint32_t)__builtin_popcountll(bm & ((1ull << lid()) - 1ull));
+        n_upd += (uint32_t)__builtin_popcountll(bm);
         if (pe == PEND_NONE) continue;
-        emit_upd(ps2, (int)((pe >> 12) & 3u), (pe >> 14) & 0x3FFFu, (int)((pe >> 28) & 3u), 0u, lr_of_var(n),
+        emit_upd(k, ps2, (int)((pe >> 12) & 3u), (pe >> 14) & 0x3FFFu, (int)((pe >> 28) & 3u), 0u, lr_of_var(n),
                  1000.0 + m.gamma * 0.0, stage);
         st(slotb, slot_ix(sw2, tr), slot_make(PEND_NONE, slot_rew(slw, epoch), epoch));
       }
@@ -2013,7 +2017,11 @@ __device__ void run(const SflMap& m, const SflState& s, const SflCtl& c, const S
   }
 #endif
   if (lane == 0) {
-    if (PART) st(P->dec_done, e, dec_base + (int64_t)v.n_dec);
+    if (PART) {
+      st(P->dec_done, e, dec_base + (int64_t)v.n_dec);
+      st(P->req_dst, e, v.req_dst_v);
+      st(P->upd_n, e, v.n_upd < P->upd_env ? v.n_upd : P->upd_env);
+    }
     st(s.ep_t, e, ep_t);
     st(s.n_test, e, n_test);
     if (c.launch_dec) st(c.launch_dec, e, (uint64_t)v.n_dec);

@@ -76,7 +76,7 @@ class PartitionedBatch:
 
     def __init__(self, cm: CompiledMap, hp: dict, seeds: Sequence[int], env_base: int, envs_total: int,
                  rank: int = 0, world: int = 1, dist=None, lib: Optional[_lib.Lib] = None, device: int = 0,
-                 owner: Optional[np.ndarray] = None, upd_per_env: int = 8, ntab: Optional[int] = None,
+                 owner: Optional[np.ndarray] = None, upd_per_env: int = 16, ntab: Optional[int] = None,
                  buffer_device: str = "cuda"):
         import torch
         self.torch = torch
@@ -117,6 +117,15 @@ class PartitionedBatch:
         self.on_gpu = dev.type == "cuda"
         self.rec = (rq.value, rp.value, up.value)
         self.rounds = 0
+        self._counts = (C.c_uint32 * (2 * self.world + 1))()
+        self.stream = None
+        if self.on_gpu:
+            # the round's kernels, copies and collectives queue on one stream (torch's, inside
+            # step()), so the owner steps need no host synchronisation: one per round, for the counts
+            torch.cuda.current_stream().synchronize()
+            self.stream = torch.cuda.Stream(device=dev)
+            self.lib.check(self.lib.dll.sfl_set_stream(self.batch.h, C.c_void_p(self.stream.cuda_stream)),
+                           "sfl_set_stream")
 
     def close(self):
         self.batch.close()
@@ -152,36 +161,28 @@ class PartitionedBatch:
 
     # ---- one part step: every env makes `decisions_per_env` decisions ---------------------------
     def _exchange(self, recv, send):
-        if recv is send:
-            return
-        if self.dist is None or self.world == 1:
+        """One rank: every segment is addressed to this rank (the receive buffers are the send buffers)."""
+        if recv is not send:
             recv.copy_(send)
-        elif recv.is_cuda and self.dist.get_backend() == "gloo":
-            # gloo (multi-rank rehearsal on one GPU): exchange through host memory
-            r = self.torch.empty_like(recv, device="cpu")
-            self.dist.all_to_all_single(r, send.cpu())
-            recv.copy_(r)
-        else:
-            self.dist.all_to_all_single(recv, send)
-        if self.on_gpu:
-            self.torch.cuda.current_stream().synchronize()
 
-    # ---- size-aware exchange (N > 1 ranks on NCCL/RCCL, or gloo with host buffers) ------------------
+    # ---- size-aware exchange (N > 1 ranks) ----------------------------------------------------------
     # Each destination segment's filled prefix (header record + its records) travels as one
     # point-to-point message into the same place of the receiver's segment: the owner kernels
-    # read a segment only up to its header count, so nothing beyond the prefix is needed.
+    # read a segment only up to its header count, so nothing beyond the prefix is needed.  On
+    # NCCL/RCCL the messages go device to device; gloo (the multi-rank rehearsal with GPU buffers on
+    # one box, or host buffers) stages each prefix through host memory.
     def _sized(self) -> bool:
-        return self.dist is not None and self.world > 1 and not (self.on_gpu and self.dist.get_backend() == "gloo")
+        return self.dist is not None and self.world > 1
 
-    def _header_counts(self, buf, cap, rec):
-        seg = buf.view(self.world, (cap + 1) * rec)
-        return seg[:, :4].contiguous().view(self.torch.int32).reshape(self.world).to(self.torch.int64)
+    def _host_staged(self) -> bool:
+        return self.on_gpu and self.dist.get_backend() == "gloo"
 
     def _p2p(self, recv, send, cap, rec, n_send, n_recv):
         torch, dist = self.torch, self.dist
         rs, ss = recv.view(self.world, (cap + 1) * rec), send.view(self.world, (cap + 1) * rec)
-        ops = []
+        ops, landing = [], []
         row = (cap + 1) * rec
+        staged = self._host_staged()
         for p in range(self.world):
             k_s, k_r = (int(n_send[p]) + 1) * rec, (int(n_recv[p]) + 1) * rec
             if k_s > row or k_r > row:
@@ -189,36 +190,50 @@ class PartitionedBatch:
             if p == self.rank:
                 rs[p, :k_r].copy_(ss[p, :k_s])
                 continue
-            ops.append(dist.P2POp(dist.isend, ss[p, :k_s], p))
-            ops.append(dist.P2POp(dist.irecv, rs[p, :k_r], p))
+            if staged:
+                r = torch.empty(k_r, dtype=torch.uint8)
+                landing.append((rs[p, :k_r], r))
+                ops.append(dist.P2POp(dist.isend, ss[p, :k_s].cpu(), p))
+                ops.append(dist.P2POp(dist.irecv, r, p))
+            else:
+                ops.append(dist.P2POp(dist.isend, ss[p, :k_s], p))
+                ops.append(dist.P2POp(dist.irecv, rs[p, :k_r], p))
         if ops:
             for r in dist.batch_isend_irecv(ops):
                 r.wait()
-        if self.on_gpu:
-            torch.cuda.current_stream().synchronize()
+        for dst, r in landing:
+            dst.copy_(r)
+
+    def _local_counts(self):
+        """(requests, update records) per destination and the highest update stage of this rank's
+        last sfl_part_local (host copies: no device read)."""
+        w = self.world
+        self.lib.check(self.lib.dll.sfl_part_counts(self.batch.h, self._counts, 2 * w + 1), "sfl_part_counts")
+        c = list(self._counts)
+        return c[:w], c[w:2 * w], c[2 * w]
 
     def _exchange_sized(self, err: int = 0):
         """Updates and requests: counts first (one small all-to-all, which also carries this rank's
-        error flag to every rank), then the filled prefixes.  Returns the job-wide error flag; on an
-        error nothing else is exchanged (every rank stops at the same point)."""
+        error flag and highest update stage to every rank), then the filled prefixes.  Returns the
+        job-wide error flag; on an error nothing else is exchanged (every rank stops at the same point)."""
         torch = self.torch
         rq, _, up = self.rec
         if err:
-            n_req = torch.zeros(self.world, dtype=torch.int64, device=self.req_send.device)
-            n_upd = n_req
+            n_req, n_upd, mst = [0] * self.world, [0] * self.world, 0
         else:
-            n_req = self._header_counts(self.req_send, self.cap_req, rq)
-            n_upd = self._header_counts(self.upd_send, self.cap_upd, up)
-        fl = torch.full_like(n_req, int(err))
-        cs = torch.stack([n_req, n_upd, fl], dim=1).contiguous()  # row d: what this rank sends to rank d
+            n_req, n_upd, mst = self._local_counts()
+        # row d: what this rank sends to rank d
+        dev = "cpu" if self.dist.get_backend() == "gloo" else self.req_send.device
+        cs = torch.tensor([[n_req[d], n_upd[d], int(err), mst] for d in range(self.world)], dtype=torch.int64, device=dev)
         cr = torch.empty_like(cs)
         self.dist.all_to_all_single(cr, cs)                    # row s: what rank s sends to this rank
-        cs, cr = cs.cpu().tolist(), cr.cpu().tolist()
+        cr = cr.cpu().tolist()
         if any(c[2] for c in cr):
             return 1
-        self._n_req_sent = [c[0] for c in cs]
+        self._max_stage = max(c[3] for c in cr)
+        self._n_req_sent = list(n_req)
         self._n_req_recv = [c[0] for c in cr]
-        self._p2p(self.upd_recv, self.upd_send, self.cap_upd, up, [c[1] for c in cs], [c[1] for c in cr])
+        self._p2p(self.upd_recv, self.upd_send, self.cap_upd, up, n_upd, [c[1] for c in cr])
         self._p2p(self.req_recv, self.req_send, self.cap_req, rq, self._n_req_sent, self._n_req_recv)
         return 0
 
@@ -230,6 +245,12 @@ class PartitionedBatch:
     def step(self, decisions_per_env: int) -> int:
         """Advance every local env by ``decisions_per_env`` learning decisions (the sfl_step contract);
         returns the number of rounds.  Collective over the ranks."""
+        if self.stream is None:
+            return self._step(decisions_per_env)
+        with self.torch.cuda.stream(self.stream):
+            return self._step(decisions_per_env)
+
+    def _step(self, decisions_per_env: int) -> int:
         d = self.lib.dll
         h = self.batch.h
         ptr = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
@@ -253,7 +274,10 @@ class PartitionedBatch:
             if failed:
                 raise _lib.SflError(f"rank {self.rank}: sfl_part_local: " +
                                     (msg or "stopped because another rank failed"))
-            self.lib.check(d.sfl_part_update(h, ptr(self.upd_recv)), "sfl_part_update")
+            if sized:  # the senders' highest stage came with the counts: no header read
+                self.lib.check(d.sfl_part_update_stages(h, ptr(self.upd_recv), self._max_stage), "sfl_part_update")
+            else:
+                self.lib.check(d.sfl_part_update(h, ptr(self.upd_recv)), "sfl_part_update")
             self.lib.check(d.sfl_part_answer(h, ptr(self.req_recv), ptr(self.rep_send)), "sfl_part_answer")
             if sized:
                 self._exchange_replies_sized()
