@@ -88,52 +88,65 @@ __global__ void __launch_bounds__(256) k_part_local(const sfl::SflMap* __restric
 // lane-per-env kernel wrote the segments itself; only the totals.
 __global__ void __launch_bounds__(256) k_part_compact(const sfl::SflPart* __restrict__ P, const sfl::SflState* __restrict__ s,
                                                       const sfl::SflCtl* __restrict__ c, int dense) {
-  constexpr int MAXU = 32;  // sfl_part_config caps upd_env
+  constexpr int MAXU = sfl::PART_UPD_ENV_MAX;  // (register arrays: the loops over them are unrolled)
   __shared__ uint32_t lreq[256], lupd[256], breq[256], bupd[256];
-  __shared__ unsigned long long lsum[3];
-  __shared__ uint32_t lerr, lmax;
+  __shared__ unsigned long long lsum[4][4];
+  __shared__ uint32_t lmax;
   const int world = P->world;
   for (int i = threadIdx.x; i < world; i += blockDim.x) lreq[i] = lupd[i] = 0u;
-  if (threadIdx.x == 0) {
-    lsum[0] = lsum[1] = lsum[2] = 0ull;
-    lerr = lmax = 0u;
-  }
+  if (threadIdx.x == 0) lmax = 0u;
   __syncthreads();
   const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
   const bool valid = e < s->E;
   int rd = -1;
-  uint32_t kr = 0, nu = 0, ku[MAXU];
-  uint8_t du[MAXU];
-  if (valid) {
-    if (!dense) {
-      rd = P->req_dst[e];
-      if (rd >= 0) kr = atomicAdd(&lreq[rd], 1u);
-      nu = P->upd_n[e];
-      for (uint32_t i = 0; i < nu && i < (uint32_t)MAXU; ++i) {
+  uint32_t kr = 0, nu = 0, ku[MAXU], du[MAXU], mst = 0;
+  if (valid && !dense) {
+    rd = P->req_dst[e];
+    if (rd >= 0) kr = atomicAdd(&lreq[rd], 1u);
+    nu = P->upd_n[e];
+#pragma unroll
+    for (int i = 0; i < MAXU; ++i) {
+      if ((uint32_t)i < nu) {
         const sfl::PartUpd& u = P->upd_st[(size_t)e * P->upd_env + i];
-        const int d = P->owner[u.port >> 2];
-        du[i] = (uint8_t)d;
-        ku[i] = atomicAdd(&lupd[d], 1u);
-        atomicMax(&lmax, (uint32_t)u.stage);
+        du[i] = (uint32_t)P->owner[u.port >> 2];
+        ku[i] = atomicAdd(&lupd[du[i]], 1u);
+        mst = u.stage > mst ? u.stage : mst;
       }
     }
-    atomicAdd(&lsum[0], (unsigned long long)c->launch_dec[e]);
-    atomicAdd(&lsum[1], (unsigned long long)c->launch_ticks[e]);
-    atomicAdd(&lsum[2], (unsigned long long)c->launch_bytes[e]);
-    atomicOr(&lerr, s->err[e]);
+  }
+  // the envs' launch totals: wave sums, then one LDS slot per wave
+  unsigned long long a = valid ? c->launch_dec[e] : 0ull, b = valid ? c->launch_ticks[e] : 0ull,
+                     d = valid ? c->launch_bytes[e] : 0ull, o = valid ? s->err[e] : 0ull;
+  for (int off = 32; off > 0; off >>= 1) {
+    a += __shfl_xor(a, off, 64);
+    b += __shfl_xor(b, off, 64);
+    d += __shfl_xor(d, off, 64);
+    o |= __shfl_xor(o, off, 64);
+    mst = max(mst, (uint32_t)__shfl_xor((int)mst, off, 64));
+  }
+  if ((threadIdx.x & 63) == 0) {
+    const int w = threadIdx.x >> 6;
+    lsum[w][0] = a;
+    lsum[w][1] = b;
+    lsum[w][2] = d;
+    lsum[w][3] = o;
+    atomicMax(&lmax, mst);
   }
   __syncthreads();
   for (int i = threadIdx.x; i < world; i += blockDim.x) {
     breq[i] = lreq[i] ? atomicAdd(P->cnt + i, lreq[i]) : 0u;
     bupd[i] = lupd[i] ? atomicAdd(P->cnt + world + i, lupd[i]) : 0u;
   }
-  if (threadIdx.x == 0) {
-    atomicAdd((unsigned long long*)&P->sums[0], lsum[0]);
-    atomicAdd((unsigned long long*)&P->sums[1], lsum[1]);
-    atomicAdd((unsigned long long*)&P->sums[2], lsum[2]);
-    if (lerr) atomicOr((unsigned long long*)&P->sums[3], (unsigned long long)lerr);
-    if (lmax) atomicMax(P->max_stage, lmax);
+  if (threadIdx.x < 4) {
+    unsigned long long t = 0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t = threadIdx.x == 3 ? (t | lsum[w][3]) : t + lsum[w][threadIdx.x];
+    if (threadIdx.x == 3) {
+      if (t) atomicOr((unsigned long long*)&P->sums[3], t);
+    } else {
+      atomicAdd((unsigned long long*)&P->sums[threadIdx.x], t);
+    }
   }
+  if (threadIdx.x == 0 && lmax) atomicMax(P->max_stage, lmax);
   __syncthreads();
   if (!valid || dense) return;
   uint32_t ovf = 0;
@@ -146,10 +159,13 @@ __global__ void __launch_bounds__(256) k_part_compact(const sfl::SflPart* __rest
       ovf = sfl::E_MSG_OVF;
     }
   }
-  for (uint32_t i = 0; i < nu && i < (uint32_t)MAXU; ++i) {
-    const uint32_t d = du[i], k = bupd[d] + ku[i];
-    if (k < P->cap_upd) P->upd_out[(size_t)d * (P->cap_upd + 1) + 1 + k] = P->upd_st[(size_t)e * P->upd_env + i];
-    else ovf = sfl::E_MSG_OVF;
+#pragma unroll
+  for (int i = 0; i < MAXU; ++i) {
+    if ((uint32_t)i < nu) {
+      const uint32_t k = bupd[du[i]] + ku[i];
+      if (k < P->cap_upd) P->upd_out[(size_t)du[i] * (P->cap_upd + 1) + 1 + k] = P->upd_st[(size_t)e * P->upd_env + i];
+      else ovf = sfl::E_MSG_OVF;
+    }
   }
   if (ovf) {
     s->err[e] |= ovf;

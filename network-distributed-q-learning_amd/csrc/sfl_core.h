@@ -206,6 +206,16 @@ SFL_FN uint32_t sem_in(uint64_t r) { return (uint32_t)((r >> 40) & 1ull); }
 SFL_FN uint64_t sem_retime(uint64_t r, uint32_t owner, int32_t t0, int32_t t1) {
   return sem_pack(owner, sem_in(r), t0, t1);
 }
+// the wavefront kernels' 32-bit record (LDS, and their env-major state between launches):
+// t0 14 (signed) | t1 - t0 9 | owner 7 | in 1 | present 1 (choose_variant checks that the map's
+// ticks and spans fit)
+constexpr uint32_t R_T0_BITS = 14, R_DUR_BITS = 9, R_OWNER_SHIFT = R_T0_BITS + R_DUR_BITS;
+constexpr uint32_t R_T0_MASK = (1u << R_T0_BITS) - 1u, R_DUR_MASK = (1u << R_DUR_BITS) - 1u;
+SFL_FN uint64_t wave_rec_to64(uint32_t r) {
+  if (!(r >> 31)) return 0ull;
+  const int32_t t0 = ((int32_t)(r << (32 - R_T0_BITS))) >> (32 - R_T0_BITS);
+  return sem_pack((r >> R_OWNER_SHIFT) & 0x7Fu, (r >> 30) & 1u, t0, t0 + (int32_t)((r >> R_T0_BITS) & R_DUR_MASK));
+}
 
 // (switch, train) slot: pending 32 | reward 24 (signed) | epoch 8
 SFL_FN uint32_t slot_pend(uint64_t v, uint32_t epoch) { return ((uint32_t)(v >> 56) == (epoch & 0xFFu)) ? (uint32_t)v : PEND_NONE; }

@@ -602,7 +602,7 @@ int part_config(Handle<B>* h, int rank, int world, const int32_t* owner, uint32_
   if (cap_req >= (1u << 24) || cap_upd < 1) return fail("sfl_part_config: bad capacities");
   // the wave kernel stages up to upd_env update records per env and round (E_MSG_OVF beyond); the
   // segments must hold every env's staged records
-  const uint32_t upd_env = cap_upd / h->E < 32u ? cap_upd / h->E : 32u;
+  const uint32_t upd_env = cap_upd / h->E < PART_UPD_ENV_MAX ? cap_upd / h->E : PART_UPD_ENV_MAX;
   if (upd_env < 2) return fail("sfl_part_config: update capacity must allow two records per local env");
   const int S = h->map.S, K = h->map.K;
   std::vector<int32_t> own(owner, owner + S);

@@ -23,6 +23,7 @@ namespace sfl {
 
 enum : uint32_t { F_REQ = 64 };  // eflags: a request is waiting for its reply
 enum : uint32_t { E_MSG_OVF = 16 };  // a message segment overflowed (capacity too small)
+constexpr uint32_t PART_UPD_ENV_MAX = 16;  // staged update records per env and round, at most
 
 // message records; record 0 of each destination segment is a header whose first word is the
 // number of records that follow

@@ -116,10 +116,9 @@ __device__ __forceinline__ uint32_t rl(uint32_t v, int lane) {
 }
 __device__ __forceinline__ int32_t rl(int32_t v, int lane) { return (int32_t)__builtin_amdgcn_readlane((int)v, lane); }
 
-// semaphore record in a VGPR / LDS word: t0 14 (signed) | t1 - t0 9 | owner 7 | in 1 | present 1
-// (ticks -8192..8191 and spans up to 511: choose_variant checks the map's timetable and port lengths)
-constexpr uint32_t R_T0_BITS = 14, R_DUR_BITS = 9, R_OWNER_SHIFT = R_T0_BITS + R_DUR_BITS;
-constexpr uint32_t R_T0_MASK = (1u << R_T0_BITS) - 1u, R_DUR_MASK = (1u << R_DUR_BITS) - 1u;
+// semaphore record in a VGPR / LDS word and in the env-major state between launches (R_* in
+// sfl_core.h): t0 14 (signed) | t1 - t0 9 | owner 7 | in 1 | present 1 (ticks -8192..8191 and
+// spans up to 511: choose_variant checks the map's timetable and port lengths)
 __device__ __forceinline__ uint32_t r_pack(uint32_t owner, uint32_t in, int32_t t0, int32_t t1) {
   return ((uint32_t)t0 & R_T0_MASK) | (((uint32_t)(t1 - t0) & R_DUR_MASK) << R_T0_BITS) | ((owner & 0x7Fu) << R_OWNER_SHIFT) |
          ((in & 1u) << 30) | (1u << 31);
@@ -132,9 +131,6 @@ __device__ __forceinline__ uint32_t r_dur(uint32_t r) { return (r >> R_T0_BITS) 
 __device__ __forceinline__ int32_t r_t1(uint32_t r) { return r_t0(r) + (int32_t)r_dur(r); }
 // the same record restarted at tick t (extend_semaphores: span kept)
 __device__ __forceinline__ uint32_t r_retime(uint32_t r, int32_t t) { return (r & ~R_T0_MASK) | ((uint32_t)t & R_T0_MASK); }
-__device__ __forceinline__ uint32_t r_from64(uint64_t x) {
-  return sem_present(x) ? r_pack(sem_owner(x), sem_in(x), sem_t0(x), sem_t1(x)) : 0u;
-}
 __device__ __forceinline__ uint64_t r_to64(uint32_t r) {
   return r_present(r) ? sem_pack(r_owner(r), r_in(r), r_t0(r), r_t1(r)) : 0ull;
 }
@@ -311,6 +307,7 @@ struct WEnv {
   // PART: this launch's messages, staged in the env's own slots (k_part_compact packs them)
   int32_t req_dst_v = -1;  // destination of the request (-1: none)
   uint32_t n_upd = 0;      // update records staged
+  uint32_t sem0[PART ? PPL : 1], cnt0[PART ? SPL : 1];  // the launch's loaded records / counters
 #ifdef SFL_PROFILE
   uint64_t prof[9] = {};  // decide: observe, epsilon-greedy, apply; events: prefetch, row hit/miss, pend hit/miss, decisions
   uint64_t lap[16] = {};  // finer segments (see SFL_LAP call sites)
@@ -344,6 +341,9 @@ struct WEnv {
   // body keeps the env index fastest instead)
   __device__ __forceinline__ size_t tix(int h) const { return (size_t)e * (uint32_t)m.T + (uint32_t)h; }
   __device__ __forceinline__ size_t pix(int p) const { return (size_t)e * (uint32_t)m.NP + (uint32_t)p; }
+  // the semaphore state between launches: 32-bit records, env-major (the array is sized for the
+  // lane-per-env body's 64-bit ones)
+  __device__ __forceinline__ uint32_t* sem_words() const { return (uint32_t*)s.sem; }
   __device__ __forceinline__ size_t cix(int sw) const { return (size_t)e * (uint32_t)m.S + (uint32_t)sw; }
 
   // ---- group primitives -------------------------------------------------------------
@@ -665,12 +665,16 @@ struct WEnv {
 #pragma unroll
     for (int k = 0; k < PPL; ++k) {
       const int p = k * G + lane;
-      sem(k) = p < m.NP ? r_from64(ld(s.sem, pix(p))) : 0u;
+      const uint32_t r = p < m.NP ? ld(sem_words(), pix(p)) : 0u;
+      sem(k) = r;
+      if constexpr (PART) sem0[k] = r;
     }
 #pragma unroll
     for (int k = 0; k < SPL; ++k) {
       const int sw = k * G + lane;
-      lcnt[k * G + lane] = sw < m.S ? ld(s.counts, cix(sw)) : 0u;
+      const uint32_t n = sw < m.S ? ld(s.counts, cix(sw)) : 0u;
+      lcnt[k * G + lane] = n;
+      if constexpr (PART) cnt0[k] = n;
     }
     now = U(ld(s.elapsed, e));
     flags = U(ld(s.eflags, e));
@@ -711,15 +715,16 @@ struct WEnv {
         st(s.tr_delay, tix(hk), delay[k]);
       }
     }
+    // (PART: a round changes a handful of records and one counter; only those are written back)
 #pragma unroll
     for (int k = 0; k < PPL; ++k) {
       const int p = k * G + lane;
-      if (p < m.NP) st(s.sem, pix(p), r_to64(sem(k)));
+      if (p < m.NP && (!PART || sem(k) != sem0[k])) st(sem_words(), pix(p), sem(k));
     }
 #pragma unroll
     for (int k = 0; k < SPL; ++k) {
       const int sw = k * G + lane;
-      if (sw < m.S) st(s.counts, cix(sw), lcnt[k * G + lane]);
+      if (sw < m.S && (!PART || lcnt[k * G + lane] != cnt0[k])) st(s.counts, cix(sw), lcnt[k * G + lane]);
     }
     uint32_t err = 0;
 #pragma unroll

@@ -16,8 +16,11 @@ over the ranks as in the env-sharded mode.  Each round every env makes one decis
 
 Every env performs exactly the operations of the fused kernels in the same order, so the
 results are bit-identical to the single-process run (tests/test_partition.py).  Message
-buffers are fixed [world][cap + 1] record segments whose first record carries the count, so a
-round needs no host-side split sizes.
+buffers are [world][cap + 1] record segments whose first record carries the count.  On the GPU
+a round is queued on one stream (this batch's torch stream, handed to the library with
+sfl_set_stream) and synchronises once, in sfl_part_local, for the record counts; with N > 1
+ranks the counts (and each rank's highest update stage) go first, then each segment's filled
+prefix point to point.
 """
 from __future__ import annotations
 
