@@ -163,21 +163,18 @@ int sfl_part_config(sfl_handle* h, int32_t rank, int32_t world, const int32_t* o
 int sfl_part_record_sizes(uint32_t* req, uint32_t* rep, uint32_t* upd);
 int sfl_part_begin(sfl_handle* h);  /* start a part step: per-env decision counters to 0 */
 int sfl_part_local(sfl_handle* h, int64_t decisions_per_env, const void* replies, void* requests, void* updates,
-                   uint64_t* requests_sent);
+                   uint64_t* requests_sent /* null: see sfl_set_stream */);
 int sfl_part_update(sfl_handle* h, const void* updates);
-/* sfl_part_update with the highest update stage of the received segments known to the caller
- * (the maximum of the senders' sfl_part_counts[2 * world], carried by its count exchange): no
- * header read; max_stage < 0 = sfl_part_update */
-int sfl_part_update_stages(sfl_handle* h, const void* updates, int32_t max_stage);
 int sfl_part_answer(sfl_handle* h, const void* requests, void* replies);
 /* this rank's record counts of the last sfl_part_local: out[0 .. world) requests and
  * out[world .. 2 world) update records per destination, out[2 world] the highest update stage
- * (cap >= 2 * world + 1) */
+ * (cap >= 2 * world + 1); synchronises if sfl_part_local did not (and reports the envs' errors) */
 int sfl_part_counts(sfl_handle* h, uint32_t* out, int32_t cap);
 /* queue the handle's work on the caller's stream (a hipStream_t, e.g. torch's current stream,
- * which its RCCL collectives follow); then sfl_part_update / sfl_part_answer return without a
- * synchronisation and a round synchronises once, in sfl_part_local (its record counts).  null:
- * the handle's own stream again */
+ * which its RCCL collectives follow).  Then sfl_part_update / sfl_part_answer return without a
+ * synchronisation, and so does sfl_part_local when requests_sent is null (its counts are read by
+ * sfl_part_counts): a round synchronises once, for the counts, or -- one rank -- not at all.
+ * null: the handle's own stream again */
 int sfl_set_stream(sfl_handle* h, void* stream);
 /* owned Q blocks of one env of the job, written into the full per-env layout of sfl_get_q
  * (other entries untouched); owned key-set bits OR-ed into touched */

@@ -85,7 +85,6 @@ EXPORTS = {
     "sfl_part_local": (C.c_int, [C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p, P(C.c_uint64)]),
     "sfl_part_update": (C.c_int, [C.c_void_p, C.c_void_p]),
     "sfl_part_answer": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
-    "sfl_part_update_stages": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32]),
     "sfl_part_counts": (C.c_int, [C.c_void_p, P(C.c_uint32), C.c_int32]),
     "sfl_set_stream": (C.c_int, [C.c_void_p, C.c_void_p]),
     "sfl_part_get_q": (C.c_int, [C.c_void_p, C.c_uint32, P(C.c_double), P(C.c_uint32)]),

@@ -186,14 +186,40 @@ __global__ void k_part_answer(const sfl::SflMap* __restrict__ m, const sfl::SflP
   const size_t base = g * (cap + 1);
   if (k <= in[base].genv) sfl::part_answer_one(*m, *P, in[base + k], out[base + k]);
 }
+// stage 0 (the pending updates and key-set inserts: one per env and cell) in parallel; the rare
+// later stages (arrival bonuses) are listed for k_part_update_late
 __global__ void k_part_update(const sfl::SflMap* __restrict__ m, const sfl::SflPart* __restrict__ P,
-                              const sfl::PartUpd* __restrict__ in, int stage) {
+                              const sfl::PartUpd* __restrict__ in) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   const size_t cap = P->cap_upd;
   const size_t g = i / cap, k = i % cap + 1;
   if (g >= (size_t)P->world) return;
   const size_t base = g * (cap + 1);
-  if (k <= in[base].genv && in[base + k].stage == stage) sfl::part_update_one(*m, *P, in[base + k]);
+  if (k > in[base].genv) return;
+  if (in[base + k].stage == 0) sfl::part_update_one(*m, *P, in[base + k]);
+  else P->late[1 + atomicAdd(P->late, 1u)] = (uint32_t)(base + k);
+}
+// one block: the listed records stage by stage (a stage's records touch distinct cells of their
+// env; a later stage may revisit a cell), then the list is cleared for the next round
+__global__ void __launch_bounds__(1024) k_part_update_late(const sfl::SflMap* __restrict__ m, const sfl::SflPart* __restrict__ P,
+                                                           const sfl::PartUpd* __restrict__ in) {
+  const uint32_t n = P->late[0];
+  uint32_t top = 0;
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) top = max(top, (uint32_t)in[P->late[1 + i]].stage);
+  __shared__ uint32_t smax;
+  if (threadIdx.x == 0) smax = 0u;
+  __syncthreads();
+  atomicMax(&smax, top);
+  __syncthreads();
+  const uint32_t last = smax;
+  for (uint32_t st = 1; st <= last; ++st) {
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+      const sfl::PartUpd& u = in[P->late[1 + i]];
+      if (u.stage == st) sfl::part_update_one(*m, *P, u);
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) P->late[0] = 0u;
 }
 __global__ void k_replicate(uint32_t* base, size_t words, uint32_t n) {
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < words * (n - 1); i += (size_t)gridDim.x * blockDim.x)
@@ -532,14 +558,17 @@ struct HipBackend {
     k_part_answer<<<(unsigned)((n + 255) / 256), 256, 0, stream>>>(&pp->m, &pp->P, in, out);
     check(hipGetLastError(), "k_part_answer");
   }
-  void part_update(const sfl::SflMap& m, const sfl::SflPart& P, const sfl::PartUpd* in, int stage) {
+  // every stage of the received update records, without the host knowing the highest stage
+  void part_update_all(const sfl::SflMap& m, const sfl::SflPart& P, const sfl::PartUpd* in) {
     sfl::SflState s{};
     sfl::SflCtl c{};
     PartParams* pp = part_params(2, m, s, c, P);
     if (!pp) return;
     const size_t n = (size_t)P.world * P.cap_upd;
-    k_part_update<<<(unsigned)((n + 255) / 256), 256, 0, stream>>>(&pp->m, &pp->P, in, stage);
+    k_part_update<<<(unsigned)((n + 255) / 256), 256, 0, stream>>>(&pp->m, &pp->P, in);
     check(hipGetLastError(), "k_part_update");
+    k_part_update_late<<<1, 1024, 0, stream>>>(&pp->m, &pp->P, in);
+    check(hipGetLastError(), "k_part_update_late");
   }
 };
 

@@ -40,7 +40,7 @@ struct Handle {
   uint32_t last_err = 0;
   uint64_t* d_sums = nullptr;  // [4]
   bool ext_stream = false;     // the caller's stream (sfl_set_stream): owner steps queue without a sync
-  uint32_t part_max_stage = 0;            // of the last part_local
+  bool part_pending = false;              // a part_local's counts not read yet
   std::vector<uint32_t> part_counts;      // of the last part_local: [2 * world + 1]
   uint64_t* d_launch_dec = nullptr;
   uint64_t* d_launch_ticks = nullptr;
@@ -656,12 +656,15 @@ int part_config(Handle<B>* h, int rank, int world, const int32_t* owner, uint32_
   P.req_dst = h->template dalloc<int32_t>(h->E);
   P.upd_st = h->template dalloc<PartUpd>((size_t)h->E * upd_env);
   P.upd_n = h->template dalloc<uint32_t>(h->E);
+  P.late = h->template dalloc<uint32_t>(1 + (size_t)world * cap_upd);
   if (!P.owner || !P.q_own || !P.touched_own || !P.obs || !P.req_ix || !P.dec_done || !P.cnt || !P.cnt_out || !P.req_st ||
-      !P.req_dst || !P.upd_st || !P.upd_n)
+      !P.req_dst || !P.upd_st || !P.upd_n || !P.late)
     return fail("sfl_part_config: allocation failed (out of memory?)");
   P.max_stage = P.cnt + 2 * world;
   h->be.memset(P.cnt, 0, (2 * (size_t)world + 1) * 4);
   h->be.memset(P.sums, 0, 4 * 8);
+  h->be.memset(P.cnt_out, 0, 4 * 8);
+  h->be.memset(P.late, 0, 4);
   h->be.fill_f64(P.q_own, h->map.default_q, (size_t)E_tot * off);
   h->be.memset(P.touched_own, 0, (size_t)E_tot * P.own_words * 4);
   h->be.memset(P.dec_done, 0, h->E * 8);
@@ -757,10 +760,31 @@ int part_begin(Handle<B>* h) {
   return h->be.sync() ? fail(h->be.error()) : 0;
 }
 
+// the host copy of the last part_local's record counts and of the launch totals accumulated
+// since the previous read: the round's one synchronisation
+template <class B>
+int part_read(Handle<B>* h) {
+  SflPart& P = h->part;
+  std::vector<uint64_t> out(4 + (size_t)P.world + 1);
+  h->be.d2h_async(out.data(), P.cnt_out, out.size() * 8);
+  h->be.memset(P.cnt_out, 0, 4 * 8);
+  if (h->be.sync()) return fail(std::string("sfl_part_local: ") + h->be.error());
+  h->part_pending = false;
+  h->last_kernel_ms = h->be.elapsed_ms();
+  h->last_dec = out[0];
+  h->last_ticks = out[1];
+  h->last_bytes = out[2];
+  h->last_err = (uint32_t)out[3];
+  h->total_dec += out[0];
+  const uint32_t* cnt = (const uint32_t*)(out.data() + 4);
+  h->part_counts.assign(cnt, cnt + 2 * P.world + 1);
+  return scan_errors(h);
+}
+
 // local step of a round: every env applies its reply, runs to its next decision and emits the
-// request (and the update records of its post step).  One host synchronisation: the record
-// counts and the launch totals, copied behind the kernels (k_part_headers zeroes them for the
-// next round).
+// request (and the update records of its post step).  With n_req, one host synchronisation for
+// the record counts and launch totals; without it on the caller's stream (sfl_set_stream), none:
+// sfl_part_counts reads them later (errors of the envs surface there)
 template <class B>
 int part_local(Handle<B>* h, int64_t budget, const void* rep_in, void* req_out, void* upd_out, uint64_t* n_req) {
   SflPart& P = h->part;
@@ -776,30 +800,18 @@ int part_local(Handle<B>* h, int64_t budget, const void* rep_in, void* req_out, 
   c.launch_ticks = h->d_launch_ticks;
   c.launch_bytes = h->d_launch_bytes;
   float ms = 0.f;
-  int rc = h->be.part_local(h->map, h->st, c, P, h->variant, &ms);
-  std::vector<uint64_t> out(4 + (size_t)P.world + 1);
-  if (!rc) {
-    h->be.d2h_async(out.data(), P.cnt_out, out.size() * 8);
-    rc = h->be.sync();
-  }
-  if (rc) return fail(std::string("sfl_part_local: ") + h->be.error());
-  h->last_kernel_ms = h->be.elapsed_ms();
-  h->last_dec = out[0];
-  h->last_ticks = out[1];
-  h->last_bytes = out[2];
-  h->last_err = (uint32_t)out[3];
-  h->total_dec += out[0];
-  const uint32_t* cnt = (const uint32_t*)(out.data() + 4);
+  if (h->be.part_local(h->map, h->st, c, P, h->variant, &ms)) return fail(std::string("sfl_part_local: ") + h->be.error());
+  h->part_pending = true;
+  if (!n_req && h->ext_stream) return 0;
+  if (int rc = part_read(h)) return rc;
   uint64_t n = 0;
-  for (int g = 0; g < P.world; ++g) n += cnt[g];
-  h->part_max_stage = cnt[2 * P.world];
-  h->part_counts.assign(cnt, cnt + 2 * P.world + 1);
+  for (int g = 0; g < P.world; ++g) n += h->part_counts[g];
   if (n_req) *n_req = n;
-  return scan_errors(h);
+  return 0;
 }
 
 // the owner steps are queued without a synchronisation when the caller's stream carries the
-// round (sfl_set_stream): launch errors still surface, kernel faults at the next part_local
+// round (sfl_set_stream): launch errors still surface, kernel faults at the next synchronisation
 template <class B>
 int part_done(Handle<B>* h, const char* what) {
   if (h->ext_stream) return h->be.error()[0] ? fail(std::string(what) + ": " + h->be.error()) : 0;
@@ -814,27 +826,11 @@ int part_answer(Handle<B>* h, const void* req_in, void* rep_out) {
   return part_done(h, "sfl_part_answer");
 }
 
-// max_stage: the highest update stage in the received segments (every sender's part_local
-// count, carried by the caller's count exchange); < 0: read it from the segment headers (one
-// more synchronisation); one rank: this rank's own part_local count
 template <class B>
-int part_update(Handle<B>* h, const void* upd_in, int32_t max_stage = -1) {
+int part_update(Handle<B>* h, const void* upd_in) {
   SflPart& P = h->part;
   if (!P.world) return fail("sfl_part_update: handle not partitioned");
-  const PartUpd* in = (const PartUpd*)upd_in;
-  uint32_t ms = 0;
-  if (max_stage >= 0) {
-    ms = (uint32_t)max_stage;
-  } else if (P.world == 1) {
-    ms = h->part_max_stage;
-  } else {
-    std::vector<PartUpd> hd(P.world);
-    for (int g = 0; g < P.world; ++g) h->be.d2h_async(&hd[g], in + (size_t)g * (P.cap_upd + 1), sizeof(PartUpd));
-    if (h->be.sync()) return fail(h->be.error());
-    for (int g = 0; g < P.world; ++g)
-      if (hd[g].genv > 0 && hd[g].state > ms) ms = hd[g].state;
-  }
-  for (uint32_t st = 0; st <= ms; ++st) h->be.part_update(h->map, P, in, (int)st);
+  h->be.part_update_all(h->map, P, (const PartUpd*)upd_in);
   return part_done(h, "sfl_part_update");
 }
 
@@ -845,6 +841,8 @@ int part_counts(Handle<B>* h, uint32_t* out, int32_t cap) {
   if (!h->part.world) return fail("sfl_part_counts: handle not partitioned");
   const int32_t n = 2 * h->part.world + 1;
   if (cap < n) return fail("sfl_part_counts: buffer too small");
+  if (h->part_pending)
+    if (int rc = part_read(h)) return rc;
   for (int32_t i = 0; i < n; ++i) out[i] = i < (int32_t)h->part_counts.size() ? h->part_counts[i] : 0u;
   return 0;
 }

@@ -97,14 +97,21 @@ struct HostBackend {
       for (int64_t k = 1; k <= n; ++k) sfl::part_answer_one(m, P, in[base + k], out[base + k]);
     }
   }
-  void part_update(const sfl::SflMap& m, const sfl::SflPart& P, const sfl::PartUpd* in, int stage) {
+  // stage by stage up to the highest stage in the received segment headers
+  void part_update_all(const sfl::SflMap& m, const sfl::SflPart& P, const sfl::PartUpd* in) {
+    uint32_t top = 0;
     for (int g = 0; g < P.world; ++g) {
-      const size_t base = (size_t)g * (P.cap_upd + 1);
-      const int64_t n = in[base].genv;
-#pragma omp parallel for
-      for (int64_t k = 1; k <= n; ++k)
-        if (in[base + k].stage == stage) sfl::part_update_one(m, P, in[base + k]);
+      const sfl::PartUpd& hd = in[(size_t)g * (P.cap_upd + 1)];
+      if (hd.genv > 0 && hd.state > top) top = hd.state;
     }
+    for (uint32_t stage = 0; stage <= top; ++stage)
+      for (int g = 0; g < P.world; ++g) {
+        const size_t base = (size_t)g * (P.cap_upd + 1);
+        const int64_t n = in[base].genv;
+#pragma omp parallel for
+        for (int64_t k = 1; k <= n; ++k)
+          if (in[base + k].stage == stage) sfl::part_update_one(m, P, in[base + k]);
+      }
   }
 };
 

@@ -78,6 +78,8 @@ struct SflPart {
   PartUpd* upd_st;            // [E][upd_env] the env's update records of this round
   uint32_t* upd_n;            // [E] how many
   uint32_t upd_env;           // staged update records per env and round (E_MSG_OVF beyond)
+  uint32_t* late;             // [1 + world * cap_upd]: count, then the received records of stage >= 1
+                              // (applied in stage order by k_part_update_late)
   // round buffers (set per call)
   const PartRep* rep_in;      // [world][cap_req + 1]
   PartReq* req_out;           // [world][cap_req + 1]
@@ -325,16 +327,16 @@ SFL_FN void part_headers(const SflPart& P, int dst) {
 
 // after every destination's header: hand the counts and launch totals to the host copy and
 // zero them for the next round (so a round needs no separate clearing step)
+// (the counts are this round's; the launch totals accumulate until the host reads them)
 SFL_FN void part_finish(const SflPart& P) {
   uint32_t* c = (uint32_t*)(P.cnt_out + 4);
   for (int i = 0; i < 2 * P.world + 1; ++i) {
     c[i] = P.cnt[i];
     P.cnt[i] = 0u;
   }
-  for (int i = 0; i < 4; ++i) {
-    P.cnt_out[i] = P.sums[i];
-    P.sums[i] = 0ull;
-  }
+  for (int i = 0; i < 3; ++i) P.cnt_out[i] += P.sums[i];
+  P.cnt_out[3] |= P.sums[3];
+  for (int i = 0; i < 4; ++i) P.sums[i] = 0ull;
 }
 
 }  // namespace sfl

@@ -209,9 +209,10 @@ class PartitionedBatch:
 
     def _local_counts(self):
         """(requests, update records) per destination and the highest update stage of this rank's
-        last sfl_part_local (host copies: no device read)."""
+        last sfl_part_local, or None if its envs reported an error (the round's synchronisation)."""
         w = self.world
-        self.lib.check(self.lib.dll.sfl_part_counts(self.batch.h, self._counts, 2 * w + 1), "sfl_part_counts")
+        if self.lib.dll.sfl_part_counts(self.batch.h, self._counts, 2 * w + 1):
+            return None
         c = list(self._counts)
         return c[:w], c[w:2 * w], c[2 * w]
 
@@ -221,10 +222,12 @@ class PartitionedBatch:
         job-wide error flag; on an error nothing else is exchanged (every rank stops at the same point)."""
         torch = self.torch
         rq, _, up = self.rec
-        if err:
+        counts = None if err else self._local_counts()
+        if counts is None:
+            err = 1
             n_req, n_upd, mst = [0] * self.world, [0] * self.world, 0
         else:
-            n_req, n_upd, mst = self._local_counts()
+            n_req, n_upd, mst = counts
         # row d: what this rank sends to rank d
         dev = "cpu" if self.dist.get_backend() == "gloo" else self.req_send.device
         cs = torch.tensor([[n_req[d], n_upd[d], int(err), mst] for d in range(self.world)], dtype=torch.int64, device=dev)
@@ -233,7 +236,6 @@ class PartitionedBatch:
         cr = cr.cpu().tolist()
         if any(c[2] for c in cr):
             return 1
-        self._max_stage = max(c[3] for c in cr)
         self._n_req_sent = list(n_req)
         self._n_req_recv = [c[0] for c in cr]
         self._p2p(self.upd_recv, self.upd_send, self.cap_upd, up, n_upd, [c[1] for c in cr])
@@ -259,37 +261,47 @@ class PartitionedBatch:
         ptr = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
         self.lib.check(d.sfl_part_begin(h), "sfl_part_begin")
         sized = self._sized()
+        # one rank on the GPU: the rounds queue on the stream without a synchronisation; the
+        # counts (open requests, the envs' errors) are read after the last one
+        deferred = self.stream is not None and not sized
         rounds = 0
+        n_open = 0
         for _ in range(int(decisions_per_env) + 1):
             n = C.c_uint64(0)
             # a failure on one rank (error flags of its envs, message overflow) must stop every rank,
             # or the others would wait forever in the next exchange: the flag travels with the counts
             rc = d.sfl_part_local(h, int(decisions_per_env), ptr(self.rep_recv), ptr(self.req_send),
-                                  ptr(self.upd_send), C.byref(n))
-            msg = self.lib.dll.sfl_last_error().decode(errors="replace") if rc else ""
+                                  ptr(self.upd_send), None if (deferred or sized) else C.byref(n))
+            msg = d.sfl_last_error().decode(errors="replace") if rc else ""
             if sized:
                 failed = self._exchange_sized(err=1 if rc else 0)
+                if failed and not msg:
+                    msg = d.sfl_last_error().decode(errors="replace")
+                n_open = sum(self._n_req_sent) if not failed else 0
             else:
                 failed = self._any_rank(1 if rc else 0)
-                if not failed:
-                    self._exchange(self.upd_recv, self.upd_send)
-                    self._exchange(self.req_recv, self.req_send)
+                n_open = n.value
             if failed:
                 raise _lib.SflError(f"rank {self.rank}: sfl_part_local: " +
                                     (msg or "stopped because another rank failed"))
-            if sized:  # the senders' highest stage came with the counts: no header read
-                self.lib.check(d.sfl_part_update_stages(h, ptr(self.upd_recv), self._max_stage), "sfl_part_update")
-            else:
-                self.lib.check(d.sfl_part_update(h, ptr(self.upd_recv)), "sfl_part_update")
+            if not sized:
+                self._exchange(self.upd_recv, self.upd_send)
+                self._exchange(self.req_recv, self.req_send)
+            self.lib.check(d.sfl_part_update(h, ptr(self.upd_recv)), "sfl_part_update")
             self.lib.check(d.sfl_part_answer(h, ptr(self.req_recv), ptr(self.rep_send)), "sfl_part_answer")
             if sized:
                 self._exchange_replies_sized()
             else:
                 self._exchange(self.rep_recv, self.rep_send)
             rounds += 1
-        if self._any_rank(1 if n.value != 0 else 0):
+        if deferred:
+            counts = self._local_counts()
+            if counts is None:
+                raise _lib.SflError(f"rank {self.rank}: sfl_part_local: " + d.sfl_last_error().decode(errors="replace"))
+            n_open = sum(counts[0])
+        if self._any_rank(1 if n_open != 0 else 0):
             raise _lib.SflError(f"rank {self.rank}: requests still open after the last round "
-                                f"({n.value} on this rank)")
+                                f"({n_open} on this rank)")
         self.rounds += rounds
         return rounds
 
