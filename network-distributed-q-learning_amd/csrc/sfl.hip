@@ -147,7 +147,32 @@ __global__ void __launch_bounds__(256) k_part_compact(const sfl::SflPart* __rest
     }
   }
   if (threadIdx.x == 0 && lmax) atomicMax(P->max_stage, lmax);
+  // the last block to get here writes the segment headers and hands the counts and totals to the
+  // host copy (zeroing them for the next round): every block's reservations are done by then
+  __shared__ bool last;
+  __threadfence();
+  if (threadIdx.x == 0) last = atomicAdd(P->blocks_done, 1u) == gridDim.x - 1u;
   __syncthreads();
+  if (last) {
+    __threadfence();
+    uint32_t* co = (uint32_t*)(P->cnt_out + 4);
+    const uint32_t top = atomicExch(P->max_stage, 0u);
+    for (int i = threadIdx.x; i < world; i += blockDim.x) {
+      const uint32_t nr = atomicExch(P->cnt + i, 0u), nw = atomicExch(P->cnt + world + i, 0u);
+      P->req_out[(size_t)i * (P->cap_req + 1)].genv = nr < P->cap_req ? nr : P->cap_req;
+      sfl::PartUpd& hu = P->upd_out[(size_t)i * (P->cap_upd + 1)];
+      hu.genv = nw < P->cap_upd ? nw : P->cap_upd;
+      hu.state = top;
+      co[i] = nr;
+      co[world + i] = nw;
+    }
+    if (threadIdx.x == 0) {
+      co[2 * world] = top;
+      for (int i = 0; i < 3; ++i) P->cnt_out[i] += atomicExch((unsigned long long*)&P->sums[i], 0ull);
+      P->cnt_out[3] |= atomicExch((unsigned long long*)&P->sums[3], 0ull);
+      atomicExch(P->blocks_done, 0u);
+    }
+  }
   if (!valid || dense) return;
   uint32_t ovf = 0;
   if (rd >= 0) {
@@ -171,11 +196,6 @@ __global__ void __launch_bounds__(256) k_part_compact(const sfl::SflPart* __rest
     s->err[e] |= ovf;
     atomicOr((unsigned long long*)&P->sums[3], (unsigned long long)ovf);
   }
-}
-__global__ void k_part_headers(const sfl::SflPart* __restrict__ P) {
-  if ((int)threadIdx.x < P->world) sfl::part_headers(*P, (int)threadIdx.x);
-  __syncthreads();
-  if (threadIdx.x == 0) sfl::part_finish(*P);
 }
 __global__ void k_part_answer(const sfl::SflMap* __restrict__ m, const sfl::SflPart* __restrict__ P,
                               const sfl::PartReq* __restrict__ in, sfl::PartRep* __restrict__ out) {
@@ -537,8 +557,8 @@ struct HipBackend {
     else if (m.T <= 64) k_part_local<2><<<blocks, 64, 0, stream>>>(&pp->m, &pp->s, &pp->c, &pp->P);
     else k_part_local<4><<<blocks, 64, 0, stream>>>(&pp->m, &pp->s, &pp->c, &pp->P);
     if (!check(hipGetLastError(), "k_part_local")) return -1;
-    k_part_compact<<<(s.E + 255) / 256, 256, 0, stream>>>(&pp->P, &pp->s, &pp->c, variant > 0 ? 0 : 1);
-    k_part_headers<<<1, 256, 0, stream>>>(&pp->P);
+    // (64-thread blocks: a round's few records per env spread over every CU)
+    k_part_compact<<<(s.E + 63) / 64, 64, 0, stream>>>(&pp->P, &pp->s, &pp->c, variant > 0 ? 0 : 1);
     check(hipEventRecord(ev1, stream), "event");
     // (no synchronisation here: the caller issues the launch totals and the count copies behind
     // it and syncs once; *ms is read with elapsed_ms() after that)
@@ -555,7 +575,7 @@ struct HipBackend {
     PartParams* pp = part_params(1, m, s, c, P);
     if (!pp) return;
     const size_t n = (size_t)P.world * P.cap_req;
-    k_part_answer<<<(unsigned)((n + 255) / 256), 256, 0, stream>>>(&pp->m, &pp->P, in, out);
+    k_part_answer<<<(unsigned)((n + 63) / 64), 64, 0, stream>>>(&pp->m, &pp->P, in, out);
     check(hipGetLastError(), "k_part_answer");
   }
   // every stage of the received update records, without the host knowing the highest stage

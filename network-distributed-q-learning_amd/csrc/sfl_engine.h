@@ -648,7 +648,7 @@ int part_config(Handle<B>* h, int rank, int world, const int32_t* owner, uint32_
   P.obs = h->template dalloc<Obs>(h->E);
   P.req_ix = h->template dalloc<uint32_t>(h->E);
   P.dec_done = h->template dalloc<int64_t>(h->E);
-  P.cnt = h->template dalloc<uint32_t>(2 * (size_t)world + 1);
+  P.cnt = h->template dalloc<uint32_t>(2 * (size_t)world + 2);
   P.sums = h->d_sums;
   P.cnt_out = h->template dalloc<uint64_t>(4 + (size_t)world + 1);
   P.upd_env = upd_env;
@@ -661,7 +661,8 @@ int part_config(Handle<B>* h, int rank, int world, const int32_t* owner, uint32_
       !P.req_dst || !P.upd_st || !P.upd_n || !P.late)
     return fail("sfl_part_config: allocation failed (out of memory?)");
   P.max_stage = P.cnt + 2 * world;
-  h->be.memset(P.cnt, 0, (2 * (size_t)world + 1) * 4);
+  P.blocks_done = P.cnt + 2 * world + 1;
+  h->be.memset(P.cnt, 0, (2 * (size_t)world + 2) * 4);
   h->be.memset(P.sums, 0, 4 * 8);
   h->be.memset(P.cnt_out, 0, 4 * 8);
   h->be.memset(P.late, 0, 4);

@@ -68,6 +68,7 @@ struct SflPart {
   int64_t* dec_done;          // [E] decisions since sfl_part_begin
   uint32_t* cnt;              // [2][world] records emitted this round (requests, updates)
   uint32_t* max_stage;        // [1] highest update stage emitted this round
+  uint32_t* blocks_done;      // [1] k_part_compact's finished blocks (the last one writes the headers)
   uint64_t* sums;             // [4] this round's launch totals (decisions, ticks, bytes, error bits OR)
   uint64_t* cnt_out;          // [4 + world + 1]: sums, then the [2 * world + 1] counts (incl. max_stage) as
                               // u32: the one host read of a round (part_finish zeroes cnt / sums for the next)
