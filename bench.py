@@ -142,6 +142,9 @@ def main():
     ap.add_argument("--config", default="c3")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--remote-rows", action="store_true",
+                    help="with --partition: every row operation travels as a message, also those on the rank's own "
+                         "switches (the message path measured on one rank)")
     ap.add_argument("--partition", action="store_true",
                     help="graph-partitioned mode (BASELINE configs[4]): switch agents owned by ranks, RCCL all-to-all "
                          "of row lookups and updates; defaults to --config c5 --envs 16384 (238 GB of owned Q rows per GPU)")
@@ -251,7 +254,7 @@ def bench_partition(args):
     seeds = par.shard_seeds(450565, E, rank)
     importlib.import_module(PKG + ".build").build_hip()
     pb = part.PartitionedBatch(cm, HP, seeds, rank * E, world * E, rank=rank, world=world, dist=dist, device=dev,
-                               buffer_device="cuda")
+                               buffer_device="cuda", local_rows=not args.remote_rows)
     pb.learn_begin()
     pb.apply_qinit()
     for _ in range(args.warmup):
@@ -287,7 +290,10 @@ def bench_partition(args):
             "data": f"synthetic {cm.S}-switch/{cm.T}-train Flatland-format map (mapgen {cfg}, seed 450565)",
             "config": {"workload": f"{cfg}: {cm.S} switches / {cm.T} trains, switch agents graph-partitioned over "
                                    f"{world} rank(s) (BFS blocks, cut {part.cut_fraction(cm, pb.owner):.2f}), {E} envs "
-                                   f"per GPU, {args.decisions} agent-env-steps per env per step",
+                                   f"per GPU, {args.decisions} agent-env-steps per env per step, "
+                                   + ("every row operation as a message" if args.remote_rows else
+                                      "own rows in place, other ranks' rows as messages"),
+                       "local_rows": not args.remote_rows,
                        "envs_per_gpu": E, "decisions_per_env_per_step": args.decisions,
                        "rounds_per_step": rounds / max(1, args.steps),
                        "parallelism": f"env-batch dp{world} x switch-agent partition {world}"},

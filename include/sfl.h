@@ -176,6 +176,11 @@ int sfl_part_counts(sfl_handle* h, uint32_t* out, int32_t cap);
  * sfl_part_counts): a round synchronises once, for the counts, or -- one rank -- not at all.
  * null: the handle's own stream again */
 int sfl_set_stream(sfl_handle* h, void* stream);
+/* 1 (default): the wave kernel decides on and updates the rows of this rank's own switches
+ * directly, and only rows owned by other ranks travel as requests / update records (one rank:
+ * no messages at all); 0: every row operation goes through the owner's messages, as in the
+ * lane-per-env body (the message path measured on one rank).  Results are identical. */
+int sfl_part_set_local_rows(sfl_handle* h, int32_t on);
 /* owned Q blocks of one env of the job, written into the full per-env layout of sfl_get_q
  * (other entries untouched); owned key-set bits OR-ed into touched */
 int sfl_part_get_q(sfl_handle* h, uint32_t global_env, double* q, uint32_t* touched);

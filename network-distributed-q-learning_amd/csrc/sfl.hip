@@ -67,8 +67,11 @@ k_wave_part(const sfl::SflMap* __restrict__ m, const sfl::SflState* __restrict__
             const sfl::SflPart* __restrict__ P) {
   sfl::wave::run<PPL, SPL, TW, false, true>(*m, *s, *c, P);
 }
+#ifndef SFL_WAVE2P_OCC
+#define SFL_WAVE2P_OCC 3  // k_wave2_part: 5.2 KB of LDS per env, so the registers set its occupancy
+#endif
 template <int PPL, int SPL, int TW>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SFL_WAVE2_OCC)))
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SFL_WAVE2P_OCC)))
 k_wave2_part(const sfl::SflMap* __restrict__ m, const sfl::SflState* __restrict__ s, const sfl::SflCtl* __restrict__ c,
              const sfl::SflPart* __restrict__ P) {
   sfl::wave::run<PPL, SPL, TW, false, true>(*m, *s, *c, P);

@@ -633,6 +633,7 @@ int part_config(Handle<B>* h, int rank, int world, const int32_t* owner, uint32_
   SflPart& P = h->part;
   P.rank = rank;
   P.world = world;
+  P.local_rows = 1;
   P.env_base = env_base;
   P.E_tot = E_tot;
   P.cap_req = cap_req;
@@ -833,6 +834,16 @@ int part_update(Handle<B>* h, const void* upd_in) {
   if (!P.world) return fail("sfl_part_update: handle not partitioned");
   h->be.part_update_all(h->map, P, (const PartUpd*)upd_in);
   return part_done(h, "sfl_part_update");
+}
+
+// whether the wave kernel decides and updates the rows of this rank's own switches directly (1,
+// the default) or sends every row operation through the owner's messages (0, e.g. to measure the
+// message path on one rank); the lane-per-env body always sends
+template <class B>
+int part_set_local_rows(Handle<B>* h, int on) {
+  if (!h->part.world) return fail("sfl_part_set_local_rows: handle not partitioned");
+  h->part.local_rows = on ? 1 : 0;
+  return 0;
 }
 
 // this rank's record counts of the last part_local: [2 * world + 1] = requests per destination,

@@ -53,6 +53,7 @@ static_assert(sizeof(PartReq) == 16 && sizeof(PartRep) == 16 && sizeof(PartUpd) 
 
 struct SflPart {
   int32_t rank, world;
+  int32_t local_rows;         // the wave kernel reads / writes this rank's own rows directly (no message)
   uint32_t env_base;  // global index of local env 0
   uint32_t E_tot;     // envs over all ranks
   uint32_t cap_req, cap_upd;  // records per destination segment (without the header)

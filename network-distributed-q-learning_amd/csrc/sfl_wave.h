@@ -257,6 +257,9 @@ struct WEnv {
   const int gbase;  // first wavefront lane of the group
   const SflPart* P;  // PART only
   static constexpr int TPL = (TWc + G - 1) / G;  // train slots per lane: trains lane, lane + G, ...
+  // prefetch records: one per queued train; PART stages only the train that decides in the launch
+  static constexpr int PF_SLOTS = PART ? 1 : TWc;
+  __device__ __forceinline__ static int pfx(int h) { return PART ? 0 : h; }
   static constexpr int kG = G;
   static_assert(TPL * G <= 128, "at most 128 train slots per env");
   using Mask = typename MaskOf<(TWc <= 32 ? 32 : TPL * G)>::type;
@@ -307,6 +310,7 @@ struct WEnv {
   // PART: this launch's messages, staged in the env's own slots (k_part_compact packs them)
   int32_t req_dst_v = -1;  // destination of the request (-1: none)
   uint32_t n_upd = 0;      // update records staged
+  uint32_t stg = 0;        // next update stage of this launch (the posts' records in program order)
   uint32_t sem0[PART ? PPL : 1], cnt0[PART ? SPL : 1];  // the launch's loaded records / counters
 #ifdef SFL_PROFILE
   uint64_t prof[9] = {};  // decide: observe, epsilon-greedy, apply; events: prefetch, row hit/miss, pend hit/miss, decisions
@@ -325,12 +329,21 @@ struct WEnv {
       mine[k] = lane + G * k < m_.T;
       pf_roff[k] = pf_qoff[k] = PF_NONE;
     }
-    lpi = (uint32_t*)(lpf + TWc * PF_D);
-    lrng = (uint64_t*)(lds + G * (PPL + SPL) + TWc * PF_WORDS);
-    ltt = ltt_shared ? ltt_shared : (const int32_t*)(lds + G * (PPL + SPL) + TWc * PF_WORDS + 12);
-    qb = s.q + (size_t)e * m.q_per_env;
+    lpi = (uint32_t*)(lpf + PF_SLOTS * PF_D);
+    lrng = (uint64_t*)(lds + G * (PPL + SPL) + PF_SLOTS * PF_WORDS);
+    // PART: the timetable rows are read from the map (L2-resident): a launch runs one or two
+    // decisions, so a per-launch LDS copy would cost more than it saves
+    if constexpr (PART) ltt = m.tr_pack;
+    else ltt = ltt_shared ? ltt_shared : (const int32_t*)(lds + G * (PPL + SPL) + PF_SLOTS * PF_WORDS + 12);
     pf_ok = false;
-    touchb = s.touched + (size_t)e * m.touched_words;
+    if constexpr (PART) {  // the rows this rank owns, of this env (the env-local table is freed)
+      const size_t ge = (size_t)P_->env_base + e_;
+      qb = P_->q_own + ge * P_->q_own_per_env;
+      touchb = P_->touched_own + ge * P_->own_words;
+    } else {
+      qb = s.q + (size_t)e * m.q_per_env;
+      touchb = s.touched + (size_t)e * m.touched_words;
+    }
     slotb = s.slot + (size_t)e * (uint32_t)(m.S * m.T);
   }
   __device__ __forceinline__ uint32_t slot_ix(int sw, int h) const { return (uint32_t)(h * m.S + sw); }
@@ -344,6 +357,26 @@ struct WEnv {
   // the semaphore state between launches: 32-bit records, env-major (the array is sized for the
   // lane-per-env body's 64-bit ones)
   __device__ __forceinline__ uint32_t* sem_words() const { return (uint32_t*)s.sem; }
+  // PART: switch sw's agent is owned by this rank, so its rows are read and written here directly
+  // (P->local_rows; otherwise every row goes through its owner's messages)
+  __device__ __forceinline__ bool local_sw(int sw) const {
+    if constexpr (!PART) return true;
+    else return P->local_rows && LDC(P->owner, (size_t)sw) == P->rank;
+  }
+  __device__ __forceinline__ bool local_sw_var(int sw) const {  // per-lane sw
+    if constexpr (!PART) return true;
+    else return P->local_rows && ld(P->owner, (size_t)sw) == P->rank;
+  }
+  // the Q block offset / first key-set row of in-port g (group-uniform g): the map's layout, or
+  // (PART) this rank's owned table
+  __device__ __forceinline__ uint32_t qoff_of(int g, const PortRec& pr) const {
+    if constexpr (PART) return (uint32_t)LDC(P->q_off_own, (size_t)g);
+    else return pr.q_off();
+  }
+  __device__ __forceinline__ uint32_t rowb_of(int g, const PortRec& pr) const {
+    if constexpr (PART) return LDC(P->row_own, (size_t)g);
+    else return pr.row_base();
+  }
   __device__ __forceinline__ size_t cix(int sw) const { return (size_t)e * (uint32_t)m.S + (uint32_t)sw; }
 
   // ---- group primitives -------------------------------------------------------------
@@ -651,8 +684,10 @@ struct WEnv {
         nprv[k] = (uint32_t)ld(s.tr_next, tix(hk)) | ((uint32_t)ld(s.tr_prev, tix(hk)) << 16);
         sdec[k] = (uint32_t)ld(s.tr_src, tix(hk)) | ((uint32_t)ld(s.tr_dec, tix(hk)) << 16);
         delay[k] = ld(s.tr_delay, tix(hk));
-        *(vec_t<int32_t, 4>*)(ltt + 8 * hk) = ld((const vec_t<int32_t, 4>*)m.tr_pack, (size_t)hk * 2u);
-        *(vec_t<int32_t, 4>*)(ltt + 8 * hk + 4) = ld((const vec_t<int32_t, 4>*)m.tr_pack, (size_t)hk * 2u + 1u);
+        if constexpr (!PART) {
+          *(vec_t<int32_t, 4>*)(ltt + 8 * hk) = ld((const vec_t<int32_t, 4>*)m.tr_pack, (size_t)hk * 2u);
+          *(vec_t<int32_t, 4>*)(ltt + 8 * hk + 4) = ld((const vec_t<int32_t, 4>*)m.tr_pack, (size_t)hk * 2u + 1u);
+        }
       } else {
         pos[k] = -1;
         bits[k] = 0;
@@ -1179,8 +1214,8 @@ struct WEnv {
     const int slot = pin & 3;
     const int dir0 = (int)tb_dir(bits_k);
     const int pos0 = pos_k >= 0 ? pos_k : 0;
-    double* pfl = lpf + PF_D * hk;
-    uint32_t* pfi = lpi + PF_WI * hk;
+    double* pfl = lpf + PF_D * pfx(hk);
+    uint32_t* pfi = lpi + PF_WI * pfx(hk);
     // level 1: slot word, switch record, timetable row, the row block's port record, first moves
     const uint64_t slw = ld(slotb, slot_ix(sw, hk));
     const u4 w0 = sw_v4(sw, 0);
@@ -1336,7 +1371,9 @@ struct WEnv {
   // the env changed (the next launch repeats the observation, which is deterministic, and
   // applies the reply)
   __device__ __forceinline__ bool decide(Dec& d, bool greedy) {
-    const bool observe_only = PART && !(flags & F_REQ);
+    // PART: a row of this rank's own switches is decided in one pass, like the fused kernel
+    const bool loc = local_sw((int)(trl(sdec, mctz(q_mask)) >> 16));
+    const bool observe_only = PART && !(flags & F_REQ) && !loc;
     SFL_PT(t_obs);
     SFL_LAP0();
     // agent_iter: lowest queued train (switch_env.py:418-421, 616-622)
@@ -1344,7 +1381,7 @@ struct WEnv {
     // staging waits for the apply pass in the next launch)
     if (!pf_ok && !observe_only) {
       prefetch(greedy);
-      pf_ok = true;
+      pf_ok = !PART;  // (PART stages only this decision's train: the next one stages its own)
       SFL_PCNT(3);
     }
     SFL_LAP(0);
@@ -1355,8 +1392,8 @@ struct WEnv {
     const int sw = (int)(sd >> 16);
     const SwRec swr = sw_rec(sw);
     const vec_t<int32_t, 8> tr = tr_row(h);
-    const double* pfh = lpf + PF_D * h;
-    const uint32_t* pfw = lpi + PF_WI * h;
+    const double* pfh = lpf + PF_D * pfx(h);
+    const uint32_t* pfw = lpi + PF_WI * pfx(h);
     // the decision's LDS reads that do not depend on its observation, issued together: the staged
     // slot word (never stale: a decision writes only its own train's slots), row column, pending
     // cell value and distances, the epsilon-greedy stream and the switch's interaction count
@@ -1415,14 +1452,14 @@ struct WEnv {
     // issue the Q row load and the pending update's Q cell load, then draw while they fly
     const PortRec prr = port_rec(4 * sw + slot);
     const int w = prr.q_w();
-    const uint32_t roff = prr.q_off() + state * (uint32_t)w;
+    const uint32_t roff = qoff_of(4 * sw + slot, prr) + state * (uint32_t)w;
     // lane c < w holds compact column c of the row (staged by prefetch unless stale)
     const bool colv = lid() < w;
     const bool row_hit = pf_roff_h == roff;  // the staged row and its greedy choice are valid
     double v_c = 0.0;
     if (row_hit) {
       SFL_PCNT(4);
-    } else if (!PART) {
+    } else if (loc) {
       v_c = ld(qbase() + roff, (size_t)(colv ? lid() : 0));
       SFL_PCNT(5);
     }
@@ -1437,9 +1474,9 @@ struct WEnv {
       const uint32_t pstate = (pend >> 14) & 0x3FFFu;
       const int pj = (int)((pend >> 28) & 3u);
       const PortRec pr = port_rec(4 * ps + pslot);
-      d.qoff_pend = pr.q_off() + pstate * (uint32_t)pr.q_w() + (uint32_t)pj;
-      d.row_pend = pr.row_base() + pstate;
-      if (PART) {
+      d.qoff_pend = qoff_of(4 * ps + pslot, pr) + pstate * (uint32_t)pr.q_w() + (uint32_t)pj;
+      d.row_pend = rowb_of(4 * ps + pslot, pr) + pstate;
+      if (!local_sw(ps)) {
         // the pending update is applied by its row's owner
       } else if (pf_qoff_h == d.qoff_pend) {
         q_pend_v = pf_qp;
@@ -1524,7 +1561,7 @@ struct WEnv {
     // action a(c); every other action of the full row is default_q, the first of them at mind
     double mx;
     int best, arg;
-    if constexpr (PART) {
+    if (PART && !loc) {
       // the owner's reply: max over the full row, and the masked argmax (-1 for an exploratory request)
       const uint32_t ix = U(ld(P->req_ix, (size_t)e));
       const vec_t<int32_t, 4> rw =
@@ -1557,7 +1594,7 @@ struct WEnv {
       arg = (int)((rd >> (4 * ca)) & 15u);
     }
     d.mq = mx;
-    d.row_cur = prr.row_base() + state;
+    d.row_cur = rowb_of(4 * sw + slot, prr) + state;
     d.touch_cur = !explore;  // the key-set insert is done by post (one lane-0 region)
     if (!explore) action = ((amask >> best) & 1u) ? best : arg;
     // the exploratory pick comes out of the vector-ALU generator: declare the action wave-uniform,
@@ -1791,28 +1828,48 @@ struct WEnv {
     cset(d.sw, cget(d.sw) + 1u);
     SFL_LAP(10);
   }
-  // PART: post with the Q operations as update records to the rows' owners (env_post with MsgQ
-  // in sfl_part.h; stage 0 = the pending update, 1 + i = the bonus of the i-th arrived train);
-  // the decision row's key-set insert was done by its owner when it answered a greedy request
+  // PART: post with the Q operations on other ranks' rows as update records to their owners (env_post
+  // with MsgQ in sfl_part.h; stage stg = the pending update and key-set insert, stg + 1 + i = the
+  // bonus of the i-th arrived train), those on this rank's rows applied here as in post(); a
+  // greedy decision's key-set insert on a remote row was done by its owner when it answered
   __device__ __forceinline__ void post_part(const Dec& d, bool greedy) {
+    const bool loc_cur = local_sw(d.sw);
     if (greedy) {
-      if (lid() == 0) st(slotb, slot_ix(d.next_sw, d.h), slot_make(PEND_NONE, d.r_new, epoch));
+      if (lid() == 0) {
+        if (loc_cur && d.touch_cur) touch_row(d.row_cur);
+        st(slotb, slot_ix(d.next_sw, d.h), slot_make(PEND_NONE, d.r_new, epoch));
+      }
       return;
     }
     const uint32_t pend = slot_pend(d.slotword, epoch);
     const bool hp = pend != PEND_NONE;
     const int ps = hp ? (int)(pend & 0xFFFu) : 0;
+    const bool loc_p = local_sw(ps);
     const double lr = lr_of(cget(ps));
+    const double r = (double)d.reward;
+    const double target = d.sw != ps ? r + m.gamma * d.mq : r;
     // record slots taken outside the lane-0 region, so the count stays wave-uniform
+    const bool upd_rec = hp && !loc_p;
+    const bool touch_rec = hp && d.sw != ps && !d.touch_cur && !loc_cur;
     const uint32_t k0 = n_upd;
-    const bool touch_sep = hp && d.sw != ps && !d.touch_cur;
-    n_upd += (hp ? 1u : 0u) + (touch_sep ? 1u : 0u);
+    n_upd += (upd_rec ? 1u : 0u) + (touch_rec ? 1u : 0u);
+    if (stg > 254u) lerr |= E_MSG_OVF;
     if (lid() == 0) {
       if (hp) {
-        const double r = (double)d.reward;
-        const double target = d.sw != ps ? r + m.gamma * d.mq : r;
-        emit_upd(k0, ps, (int)((pend >> 12) & 3u), (pend >> 14) & 0x3FFFu, (int)((pend >> 28) & 3u), 0u, lr, target, 0);
-        if (touch_sep) emit_upd(k0 + 1u, d.sw, d.slot, d.state, 0, 1u, 0.0, 0.0, 0);
+        if (loc_p) {
+          const double a1 = (1.0 - lr) * d.q_pend;
+          const double b1 = lr * target;
+          st(qbase(), (size_t)d.qoff_pend, a1 + b1);
+          touch_row(d.row_pend);
+        } else {
+          emit_upd(k0, ps, (int)((pend >> 12) & 3u), (pend >> 14) & 0x3FFFu, (int)((pend >> 28) & 3u), 0u, lr, target,
+                   (int)stg);
+        }
+      }
+      if (loc_cur) {
+        if (d.touch_cur || (hp && d.sw != ps)) touch_row(d.row_cur);
+      } else if (touch_rec) {
+        emit_upd(k0 + (upd_rec ? 1u : 0u), d.sw, d.slot, d.state, 0, 1u, 0.0, 0.0, (int)stg);
       }
       st(slotb, slot_ix(d.sw, d.h), slot_make(PEND_NONE, slot_rew(d.slotword, epoch), epoch));
       st(slotb, slot_ix(d.next_sw, d.h),
@@ -1821,7 +1878,7 @@ struct WEnv {
     Mask fresh = arr_mask & ~fl_mask;
     fl_mask |= fresh;
     if (many(fresh)) pf_ok = false;
-    int stage = 1;
+    uint32_t stage = stg + 1u;
     while (many(fresh)) {
       const int tr = mctz(fresh);
       mclear_low(fresh);
@@ -1832,17 +1889,32 @@ struct WEnv {
         const uint32_t pe = valid ? slot_pend(slw, epoch) : PEND_NONE;
         const int ps2 = pe == PEND_NONE ? 0 : (int)(pe & 0xFFFu);
         const uint32_t n = cget_var(ps2);  // all lanes active: a bpermute reads 0 from inactive lanes
+        const bool loc2 = local_sw_var(ps2);
         // this pass's records: slots in lane order after the ones taken so far
-        const uint64_t bm = (uint64_t)BAL(pe != PEND_NONE);
+        const uint64_t bm = (uint64_t)BAL(pe != PEND_NONE && !loc2);
         const uint32_t k = n_upd + (uint32_t)__builtin_popcountll(bm & ((1ull << lid()) - 1ull));
         n_upd += (uint32_t)__builtin_popcountll(bm);
         if (pe == PEND_NONE) continue;
-        emit_upd(k, ps2, (int)((pe >> 12) & 3u), (pe >> 14) & 0x3FFFu, (int)((pe >> 28) & 3u), 0u, lr_of_var(n),
-                 1000.0 + m.gamma * 0.0, stage);
+        const int pslot = (int)((pe >> 12) & 3u);
+        const uint32_t pstate = (pe >> 14) & 0x3FFFu;
+        const int pj = (int)((pe >> 28) & 3u);
+        if (loc2) {
+          const int g = 4 * ps2 + pslot;
+          const u4 pr = port_v(g);
+          double* qp = qbase() + (uint32_t)ld(P->q_off_own, (size_t)g) + (size_t)pstate * (pr[1] >> 16) + pj;
+          const double lr2 = lr_of_var(n);
+          const double a1 = (1.0 - lr2) * ld(qp, 0);
+          const double b1 = lr2 * (1000.0 + m.gamma * 0.0);
+          st(qp, 0, a1 + b1);
+          touch_row(ld(P->row_own, (size_t)g) + pstate);
+        } else {
+          emit_upd(k, ps2, pslot, pstate, pj, 0u, lr_of_var(n), 1000.0 + m.gamma * 0.0, (int)stage);
+        }
         st(slotb, slot_ix(sw2, tr), slot_make(PEND_NONE, slot_rew(slw, epoch), epoch));
       }
       ++stage;
     }
+    stg = stage;
     cset(d.sw, cget(d.sw) + 1u);
   }
 
@@ -1868,7 +1940,8 @@ struct WEnv {
 template <int PPL, int SPL, int TW, bool TRACE, bool PART = false>
 __device__ void run(const SflMap& m, const SflState& s, const SflCtl& c, const SflPart* P = nullptr) {
   using V = WEnv<PPL, SPL, TW, PART>;
-  constexpr int LDS_WORDS = 64 * (PPL + SPL) + TW * PF_WORDS + 12 + TW * 8;  // semaphores, counters, prefetch records, rng, timetable
+  // semaphores, counters, prefetch records, rng, timetable (PART: one record, timetable from the map)
+  constexpr int LDS_WORDS = 64 * (PPL + SPL) + (PART ? 1 : TW) * PF_WORDS + 12 + (PART ? 0 : TW * 8);
   const int lane = (int)__lane_id();
   const uint32_t e = uni((uint32_t)((blockIdx.x * blockDim.x + threadIdx.x) >> 6));
   if (e >= s.E) return;
@@ -1876,6 +1949,9 @@ __device__ void run(const SflMap& m, const SflState& s, const SflCtl& c, const S
   __shared__ uint32_t lds[WPB * LDS_WORDS];
   V v(m, s, e, lane, lds + (threadIdx.x >> 6) * LDS_WORDS, P);
   v.load();
+#ifdef SFL_AB_LOAD2
+  v.load();  // timing-only tuning build: the marginal cost of the state load
+#endif
   const int64_t dec_base = PART ? (int64_t)uni((uint64_t)ld(P->dec_done, e)) : 0;
   int32_t phase = uni(ld(s.phase, e));
   int32_t ep_t = uni(ld(s.ep_t, e)), n_test = uni(ld(s.n_test, e));
@@ -2013,6 +2089,9 @@ __device__ void run(const SflMap& m, const SflState& s, const SflCtl& c, const S
     }
   }
   v.store(phase);
+#ifdef SFL_AB_STORE2
+  v.store(phase);  // timing-only tuning build: the marginal cost of the state store
+#endif
 #ifdef SFL_PROFILE
   prof[4] = (uint64_t)__builtin_amdgcn_s_memtime() - t_begin;
   if (lane == 0) {

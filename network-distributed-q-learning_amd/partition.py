@@ -80,7 +80,7 @@ class PartitionedBatch:
     def __init__(self, cm: CompiledMap, hp: dict, seeds: Sequence[int], env_base: int, envs_total: int,
                  rank: int = 0, world: int = 1, dist=None, lib: Optional[_lib.Lib] = None, device: int = 0,
                  owner: Optional[np.ndarray] = None, upd_per_env: int = 16, ntab: Optional[int] = None,
-                 buffer_device: str = "cuda"):
+                 buffer_device: str = "cuda", local_rows: bool = True):
         import torch
         self.torch = torch
         kw = {} if ntab is None else dict(ntab=ntab)
@@ -121,6 +121,11 @@ class PartitionedBatch:
         self.rec = (rq.value, rp.value, up.value)
         self.rounds = 0
         self._counts = (C.c_uint32 * (2 * self.world + 1))()
+        # rows of this rank's own switches are decided on / updated in place (no message to itself);
+        # False: every row operation travels as a message (the message path, measured on one rank)
+        self.local_rows = bool(local_rows)
+        self.lib.check(self.lib.dll.sfl_part_set_local_rows(self.batch.h, 1 if self.local_rows else 0),
+                       "sfl_part_set_local_rows")
         self.stream = None
         if self.on_gpu:
             # the round's kernels, copies and collectives queue on one stream (torch's, inside
@@ -228,14 +233,18 @@ class PartitionedBatch:
             n_req, n_upd, mst = [0] * self.world, [0] * self.world, 0
         else:
             n_req, n_upd, mst = counts
-        # row d: what this rank sends to rank d
+        # row d: what this rank sends to rank d (and, in every row, its total of requests: the job's
+        # open requests end the step)
         dev = "cpu" if self.dist.get_backend() == "gloo" else self.req_send.device
-        cs = torch.tensor([[n_req[d], n_upd[d], int(err), mst] for d in range(self.world)], dtype=torch.int64, device=dev)
+        tot = sum(n_req)
+        cs = torch.tensor([[n_req[d], n_upd[d], int(err), mst, tot] for d in range(self.world)], dtype=torch.int64,
+                          device=dev)
         cr = torch.empty_like(cs)
         self.dist.all_to_all_single(cr, cs)                    # row s: what rank s sends to this rank
         cr = cr.cpu().tolist()
         if any(c[2] for c in cr):
             return 1
+        self._job_open = sum(c[4] for c in cr)
         self._n_req_sent = list(n_req)
         self._n_req_recv = [c[0] for c in cr]
         self._p2p(self.upd_recv, self.upd_send, self.cap_upd, up, n_upd, [c[1] for c in cr])
@@ -261,9 +270,11 @@ class PartitionedBatch:
         ptr = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
         self.lib.check(d.sfl_part_begin(h), "sfl_part_begin")
         sized = self._sized()
-        # one rank on the GPU: the rounds queue on the stream without a synchronisation; the
-        # counts (open requests, the envs' errors) are read after the last one
-        deferred = self.stream is not None and not sized
+        # one rank on the GPU with every row sent as a message: the decisions+1 rounds queue on the
+        # stream without a synchronisation; the counts (open requests, the envs' errors) are read
+        # after the last one.  Otherwise each round's counts end the step as soon as no request is
+        # open anywhere (with local rows one rank needs a single round)
+        deferred = self.stream is not None and not sized and not self.local_rows
         rounds = 0
         n_open = 0
         for _ in range(int(decisions_per_env) + 1):
@@ -277,7 +288,7 @@ class PartitionedBatch:
                 failed = self._exchange_sized(err=1 if rc else 0)
                 if failed and not msg:
                     msg = d.sfl_last_error().decode(errors="replace")
-                n_open = sum(self._n_req_sent) if not failed else 0
+                n_open = self._job_open if not failed else 0
             else:
                 failed = self._any_rank(1 if rc else 0)
                 n_open = n.value
@@ -294,12 +305,14 @@ class PartitionedBatch:
             else:
                 self._exchange(self.rep_recv, self.rep_send)
             rounds += 1
+            if not deferred and n_open == 0:
+                break  # every env has made its decisions (this round's updates are applied)
         if deferred:
             counts = self._local_counts()
             if counts is None:
                 raise _lib.SflError(f"rank {self.rank}: sfl_part_local: " + d.sfl_last_error().decode(errors="replace"))
             n_open = sum(counts[0])
-        if self._any_rank(1 if n_open != 0 else 0):
+        if (not sized) and self._any_rank(1 if n_open != 0 else 0) or sized and n_open != 0:
             raise _lib.SflError(f"rank {self.rank}: requests still open after the last round "
                                 f"({n_open} on this rank)")
         self.rounds += rounds
