@@ -19,6 +19,8 @@ import os
 import sys
 import time
 
+import numpy as np
+
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 PKG = "network-distributed-q-learning_amd"
@@ -145,6 +147,10 @@ def main():
     ap.add_argument("--remote-rows", action="store_true",
                     help="with --partition: every row operation travels as a message, also those on the rank's own "
                          "switches (the message path measured on one rank)")
+    ap.add_argument("--virtual-ranks", type=int, default=0,
+                    help="with --partition on one rank: only the switches of block 0 of a V-rank partition are "
+                         "decided on in place, the rest travel as messages (a V-rank job's per-GPU traffic, without "
+                         "the transfers)")
     ap.add_argument("--partition", action="store_true",
                     help="graph-partitioned mode (BASELINE configs[4]): switch agents owned by ranks, RCCL all-to-all "
                          "of row lookups and updates; defaults to --config c5 --envs 16384 (238 GB of owned Q rows per GPU)")
@@ -253,8 +259,11 @@ def bench_partition(args):
     cm = comp.compile_scenario(mapgen.make_config(cfg))
     seeds = par.shard_seeds(450565, E, rank)
     importlib.import_module(PKG + ".build").build_hip()
+    local = not args.remote_rows
+    if args.virtual_ranks > 1 and world == 1 and local:
+        local = (part.partition_switches(cm, args.virtual_ranks) == 0).astype(np.uint8)
     pb = part.PartitionedBatch(cm, HP, seeds, rank * E, world * E, rank=rank, world=world, dist=dist, device=dev,
-                               buffer_device="cuda", local_rows=not args.remote_rows)
+                               buffer_device="cuda", local_rows=local)
     pb.learn_begin()
     pb.apply_qinit()
     for _ in range(args.warmup):
@@ -292,8 +301,10 @@ def bench_partition(args):
                                    f"{world} rank(s) (BFS blocks, cut {part.cut_fraction(cm, pb.owner):.2f}), {E} envs "
                                    f"per GPU, {args.decisions} agent-env-steps per env per step, "
                                    + ("every row operation as a message" if args.remote_rows else
+                                      f"rows of block 0 of a {args.virtual_ranks}-rank partition in place, the rest "
+                                      "as messages" if (args.virtual_ranks > 1 and world == 1) else
                                       "own rows in place, other ranks' rows as messages"),
-                       "local_rows": not args.remote_rows,
+                       "local_switches": int(pb.local_mask.sum()),
                        "envs_per_gpu": E, "decisions_per_env_per_step": args.decisions,
                        "rounds_per_step": rounds / max(1, args.steps),
                        "parallelism": f"env-batch dp{world} x switch-agent partition {world}"},

@@ -176,11 +176,13 @@ int sfl_part_counts(sfl_handle* h, uint32_t* out, int32_t cap);
  * sfl_part_counts): a round synchronises once, for the counts, or -- one rank -- not at all.
  * null: the handle's own stream again */
 int sfl_set_stream(sfl_handle* h, void* stream);
-/* 1 (default): the wave kernel decides on and updates the rows of this rank's own switches
- * directly, and only rows owned by other ranks travel as requests / update records (one rank:
- * no messages at all); 0: every row operation goes through the owner's messages, as in the
- * lane-per-env body (the message path measured on one rank).  Results are identical. */
-int sfl_part_set_local_rows(sfl_handle* h, int32_t on);
+/* Which switches' rows the wave kernel decides on and updates in place: local_switches[S] (1 = in
+ * place; only switches this rank owns), null = every switch this rank owns (the default after
+ * sfl_part_config).  The other rows travel as requests / update records to their owners -- with
+ * one rank and the default, no messages at all.  Marking fewer switches local rehearses a bigger
+ * job's message traffic on one rank (all zero: every row operation as a message, like the
+ * lane-per-env body).  Results are identical either way. */
+int sfl_part_set_local_rows(sfl_handle* h, const uint8_t* local_switches);
 /* owned Q blocks of one env of the job, written into the full per-env layout of sfl_get_q
  * (other entries untouched); owned key-set bits OR-ed into touched */
 int sfl_part_get_q(sfl_handle* h, uint32_t global_env, double* q, uint32_t* touched);

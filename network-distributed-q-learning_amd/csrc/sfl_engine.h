@@ -633,7 +633,6 @@ int part_config(Handle<B>* h, int rank, int world, const int32_t* owner, uint32_
   SflPart& P = h->part;
   P.rank = rank;
   P.world = world;
-  P.local_rows = 1;
   P.env_base = env_base;
   P.E_tot = E_tot;
   P.cap_req = cap_req;
@@ -642,6 +641,9 @@ int part_config(Handle<B>* h, int rank, int world, const int32_t* owner, uint32_
   P.own_rows = rows;
   P.own_words = (rows + 31u) / 32u;
   P.owner = h->upload(own.data(), own.size());
+  std::vector<uint32_t> loc(S);
+  for (int s = 0; s < S; ++s) loc[s] = own[s] == rank ? 1u : 0u;
+  P.local_sw = h->upload(loc.data(), loc.size());
   P.q_off_own = h->upload(qo.data(), qo.size());
   P.row_own = h->upload(ro.data(), ro.size());
   P.q_own = h->template dalloc<double>((size_t)E_tot * (off ? off : 1));
@@ -836,14 +838,26 @@ int part_update(Handle<B>* h, const void* upd_in) {
   return part_done(h, "sfl_part_update");
 }
 
-// whether the wave kernel decides and updates the rows of this rank's own switches directly (1,
-// the default) or sends every row operation through the owner's messages (0, e.g. to measure the
-// message path on one rank); the lane-per-env body always sends
+// which switches' rows the wave kernel decides on and updates directly: local[S] (null: the
+// switches this rank owns, the default), the rest through their owners' messages.  Rows of
+// another rank's switch cannot be local; marking fewer of this rank's own switches local
+// rehearses a bigger job's message traffic on one rank.  The lane-per-env body always sends.
 template <class B>
-int part_set_local_rows(Handle<B>* h, int on) {
-  if (!h->part.world) return fail("sfl_part_set_local_rows: handle not partitioned");
-  h->part.local_rows = on ? 1 : 0;
-  return 0;
+int part_set_local_rows(Handle<B>* h, const uint8_t* local) {
+  SflPart& P = h->part;
+  if (!P.world) return fail("sfl_part_set_local_rows: handle not partitioned");
+  const int S = h->map.S;
+  std::vector<int32_t> own(S);
+  h->be.d2h(own.data(), P.owner, own.size() * 4);
+  if (h->be.sync()) return fail(h->be.error());
+  std::vector<uint32_t> loc(S);
+  for (int s = 0; s < S; ++s) {
+    const bool want = local ? local[s] != 0 : own[s] == P.rank;
+    if (want && own[s] != P.rank) return fail("sfl_part_set_local_rows: switch owned by another rank marked local");
+    loc[s] = want ? 1u : 0u;
+  }
+  h->be.h2d((void*)P.local_sw, loc.data(), loc.size() * 4);
+  return h->be.sync() ? fail(h->be.error()) : 0;
 }
 
 // this rank's record counts of the last part_local: [2 * world + 1] = requests per destination,

@@ -53,7 +53,8 @@ static_assert(sizeof(PartReq) == 16 && sizeof(PartRep) == 16 && sizeof(PartUpd) 
 
 struct SflPart {
   int32_t rank, world;
-  int32_t local_rows;         // the wave kernel reads / writes this rank's own rows directly (no message)
+  const uint32_t* local_sw;   // [S] 1: the wave kernel reads / writes this switch's rows here directly
+                              // (its owner is this rank; all 0: every row operation as a message)
   uint32_t env_base;  // global index of local env 0
   uint32_t E_tot;     // envs over all ranks
   uint32_t cap_req, cap_upd;  // records per destination segment (without the header)

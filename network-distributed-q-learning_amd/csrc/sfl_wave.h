@@ -358,14 +358,14 @@ struct WEnv {
   // lane-per-env body's 64-bit ones)
   __device__ __forceinline__ uint32_t* sem_words() const { return (uint32_t*)s.sem; }
   // PART: switch sw's agent is owned by this rank, so its rows are read and written here directly
-  // (P->local_rows; otherwise every row goes through its owner's messages)
+  // (P->local_sw; otherwise its rows go through the owner's messages)
   __device__ __forceinline__ bool local_sw(int sw) const {
     if constexpr (!PART) return true;
-    else return P->local_rows && LDC(P->owner, (size_t)sw) == P->rank;
+    else return LDC(P->local_sw, (size_t)sw) != 0u;
   }
   __device__ __forceinline__ bool local_sw_var(int sw) const {  // per-lane sw
     if constexpr (!PART) return true;
-    else return P->local_rows && ld(P->owner, (size_t)sw) == P->rank;
+    else return ld(P->local_sw, (size_t)sw) != 0u;
   }
   // the Q block offset / first key-set row of in-port g (group-uniform g): the map's layout, or
   // (PART) this rank's owned table

@@ -80,7 +80,7 @@ class PartitionedBatch:
     def __init__(self, cm: CompiledMap, hp: dict, seeds: Sequence[int], env_base: int, envs_total: int,
                  rank: int = 0, world: int = 1, dist=None, lib: Optional[_lib.Lib] = None, device: int = 0,
                  owner: Optional[np.ndarray] = None, upd_per_env: int = 16, ntab: Optional[int] = None,
-                 buffer_device: str = "cuda", local_rows: bool = True):
+                 buffer_device: str = "cuda", local_rows=True):
         import torch
         self.torch = torch
         kw = {} if ntab is None else dict(ntab=ntab)
@@ -121,10 +121,19 @@ class PartitionedBatch:
         self.rec = (rq.value, rp.value, up.value)
         self.rounds = 0
         self._counts = (C.c_uint32 * (2 * self.world + 1))()
-        # rows of this rank's own switches are decided on / updated in place (no message to itself);
-        # False: every row operation travels as a message (the message path, measured on one rank)
-        self.local_rows = bool(local_rows)
-        self.lib.check(self.lib.dll.sfl_part_set_local_rows(self.batch.h, 1 if self.local_rows else 0),
+        # rows of this rank's own switches are decided on / updated in place (no message to itself).
+        # local_rows: True (all own switches), False (every row operation as a message: the message
+        # path measured on one rank) or a [S] mask of own switches (e.g. one block of a bigger job's
+        # partition: that job's message traffic rehearsed on one rank)
+        if local_rows is True:
+            mask = (self.owner == self.rank).astype(np.uint8)
+        elif local_rows is False:
+            mask = np.zeros(cm.S, np.uint8)
+        else:
+            mask = np.ascontiguousarray(local_rows, np.uint8)
+        self.local_mask = mask
+        self.local_rows = bool(mask.any())
+        self.lib.check(self.lib.dll.sfl_part_set_local_rows(self.batch.h, _ptr(mask, C.c_uint8)),
                        "sfl_part_set_local_rows")
         self.stream = None
         if self.on_gpu:
