@@ -25,6 +25,9 @@
 namespace sfl {
 namespace wave {
 
+#ifndef SFL_TICK_HOLD
+#define SFL_TICK_HOLD 2  // run_groups: ticks wait while this many groups of the wave can still decide
+#endif
 #ifdef SFL_PROFILE
 // tuning builds only: wall cycles per phase summed over waves (reset, tick, decide, post, total,
 // decide = observe + egreedy + apply)
@@ -2158,7 +2161,22 @@ __device__ void run_groups(const SflMap& m, const SflState& s, const SflCtl& c) 
   d.abytes = 0;
   const bool test_mode = c.mode == 1;
   const int64_t max_steps = m.max_steps, dec_budget = c.dec_budget;
+#ifdef SFL_PROFILE
+  // group activity of the flat loop (per wave, lane 0): iterations, and per iteration the groups
+  // that tick / post / decide, and the iterations with any tick
+  uint64_t gs[5] = {0, 0, 0, 0, 0};
+#endif
   while (true) {
+#ifdef SFL_PROFILE
+    {
+      const uint64_t bt = __ballot(phase == PH_TICK), bp = __ballot(phase == PH_POST), bd = __ballot(phase == PH_DECIDE);
+      gs[0] += 1;
+      gs[1] += (uint64_t)__builtin_popcountll(bt) / G;
+      gs[2] += (uint64_t)__builtin_popcountll(bp) / G;
+      gs[3] += (uint64_t)__builtin_popcountll(bd) / G;
+      gs[4] += (bp | bd) ? 0u : 1u;
+    }
+#endif
     if (phase == PH_RESET) {
       // learn: optional greedy round before episode t (distr_q.py:278-281)
       bool target = false;
@@ -2175,10 +2193,13 @@ __device__ void run_groups(const SflMap& m, const SflState& s, const SflCtl& c) 
       phase = PH_TICK;
     }
 #ifndef SFL_GROUP_NOSYNC
-    // tick only when no group of the wave can decide: the groups' ticks then run together (a
-    // group that needs a tick waits for the others' batches; measured 14 % faster at G = 16 than
-    // ticking each group as soon as it needs to)
-    const bool wave_decides = __ballot(phase == PH_POST || phase == PH_DECIDE) != 0ull;
+    // the groups waiting for a tick start it once fewer than SFL_TICK_HOLD groups can still
+    // decide: their ticks then run together, while the last deciding group (if any) runs its
+    // batch alongside.  Measured at G = 16 (c3): hold while >= 2 decide 1,316 M, while >= 1
+    // (ticks only when no group decides) 1,263 M, tick as soon as 3 / 2 groups wait 1,308 / 1,245 M,
+    // never hold 14 % below the second.
+    const bool wave_decides =
+        (int)__builtin_popcountll(__ballot(phase == PH_POST || phase == PH_DECIDE)) >= SFL_TICK_HOLD * G;
 #else
     const bool wave_decides = false;
 #endif
@@ -2257,6 +2278,17 @@ __device__ void run_groups(const SflMap& m, const SflState& s, const SflCtl& c) 
     }
   }
   v.store(phase);
+#ifdef SFL_PROFILE
+  {  // the counts of the group that left the loop last (it saw every iteration of the wave)
+    uint64_t mx = gs[0];
+    for (int off = 32; off > 0; off >>= 1) mx = max(mx, (uint64_t)__shfl_xor((long long)mx, off, 64));
+    const int src = __builtin_ctzll(__ballot(gs[0] == mx));
+    uint64_t w[5];
+    for (int k = 0; k < 5; ++k) w[k] = (uint64_t)__shfl((long long)gs[k], src, 64);
+    if (__lane_id() == 0)
+      for (int k = 0; k < 5; ++k) atomicAdd(&g_prof[k], (unsigned long long)w[k]);
+  }
+#endif
   if (v.lane == 0) {
     st(s.ep_t, e, ep_t);
     st(s.n_test, e, n_test);
