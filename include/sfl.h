@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define SFL_ABI_VERSION 5
+#define SFL_ABI_VERSION 6
 
 typedef struct sfl_handle sfl_handle;
 
@@ -146,6 +146,22 @@ int sfl_get_kernel_note(sfl_handle* h, char* buf, int32_t cap);
 /* read back one env's state word arrays (debug / parity tests) */
 int sfl_get_env_state(sfl_handle* h, uint32_t env, int32_t* elapsed, int32_t* phase, uint64_t* sem /* [4S] */,
                       int32_t* tr_pos /* [T] */, uint32_t* tr_bits /* [T] */);
+
+/* ---- Flatland-compatible malfunction stream ----
+ * Replaces the counter-based malfunction draw (the default, oracle/flatland_lite.py mf_draw) with
+ * a table of the proposals Flatland's ParamMalfunctionGen draws from the env's np_random each step
+ * (flatland.envs.malfunction_generators, built at test_model.py:14-19 / main.py:28-33 and
+ * reseeded by RailEnv.reset(random_seed=seed) at switch_env.py:99): table[n_envs][steps][T] =
+ * num_broken_steps proposed to train h at step t + 1 of an episode (0 = none); a proposal starts
+ * a malfunction only for a train that is not done and not already malfunctioning (the
+ * MalfunctionHandler rule).  steps == 0 returns to the counter-based draw. */
+int sfl_set_mf_schedule(sfl_handle* h, int32_t steps, const uint8_t* table);
+/* Host helper (no device): one env's table from its seeding words (flatland.utils.seeding.np_random:
+ * key = the sha512-derived init_by_array words), the timetable's randint(0, window) draws consumed
+ * at reset (flatland_patch/timetable_generators.py:115), prob = 1 - exp(-malfunction_rate),
+ * durations randint(mf_min, mf_max + 1) + 1.  out[steps][T]. */
+int sfl_mf_schedule_flatland(const uint32_t* key, int32_t nkey, const int32_t* windows, int32_t n_windows, int32_t T,
+                             double prob, int32_t mf_min, int32_t mf_max, int32_t steps, uint8_t* out);
 
 /* ---- graph-partitioned mode (BASELINE.json configs[4]; SURVEY.md §8(e) "C5") ----
  * The switch agents are partitioned over `world` ranks (owner[S]); rank r stores the Q rows of

@@ -12,7 +12,7 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 PRODUCT_LIB = os.path.join(HERE, "libsfl.so")
-ABI_VERSION = 5  # include/sfl.h SFL_ABI_VERSION
+ABI_VERSION = 6  # include/sfl.h SFL_ABI_VERSION
 
 P = C.POINTER
 
@@ -77,6 +77,10 @@ EXPORTS = {
     "sfl_get_kernel_note": (C.c_int, [C.c_void_p, C.c_char_p, C.c_int32]),
     "sfl_get_env_state": (C.c_int, [C.c_void_p, C.c_uint32, P(C.c_int32), P(C.c_int32), P(C.c_uint64),
                                     P(C.c_int32), P(C.c_uint32)]),
+    # Flatland-compatible malfunction stream (mfstream.py)
+    "sfl_set_mf_schedule": (C.c_int, [C.c_void_p, C.c_int32, P(C.c_uint8)]),
+    "sfl_mf_schedule_flatland": (C.c_int, [P(C.c_uint32), C.c_int32, P(C.c_int32), C.c_int32, C.c_int32, C.c_double,
+                                           C.c_int32, C.c_int32, C.c_int32, P(C.c_uint8)]),
     # graph-partitioned mode (partition.py)
     "sfl_part_config": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, P(C.c_int32), C.c_uint32, C.c_uint32,
                                   C.c_uint32, C.c_uint32]),

@@ -17,7 +17,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("SFL_ARCH", "gfx950")
-SOURCES = ["sfl.hip", "sfl_core.h", "sfl_wave.h", "sfl_rng.h", "sfl_engine.h", "sfl_part.h", "sfl_capi.inc", "sfl_hostsim.cpp",
+SOURCES = ["sfl.hip", "sfl_core.h", "sfl_wave.h", "sfl_rng.h", "sfl_engine.h", "sfl_part.h", "sfl_mfgen.h", "sfl_capi.inc", "sfl_hostsim.cpp",
            os.path.join("..", "..", "include", "sfl.h")]
 _MARK = re.compile(rb"SFL_BUILD_ID:([0-9a-f]{40})")
 

@@ -93,7 +93,24 @@ struct SflMap {
   const uint32_t* seedseq32;  // [2^31] first 32-bit output of Generator(PCG64(SeedSequence(v))), or null
   const uint32_t* port_tr;    // [NP][4]: transition recipe of an out port o: nb(o) | unique(nb(o)) << 16;
                               //          nb(unique) | len(o) << 16; len(unique); 0  (int16 fields, -1 = none)
+  // Flatland-compatible malfunction stream (sfl_mfgen.h): [E][mf_steps][T] num_broken_steps proposed at
+  // step t (row t - 1) of an episode, 0 = none; mf_steps == 0: the counter-based draw (mf_draw)
+  const uint8_t* mf_tab;
+  int32_t mf_steps;
 };
+
+// the malfunction proposed to train h of env e at step t, given its state and counter (both streams)
+SFL_FN uint32_t mf_propose(const SflMap& m, uint64_t seed, uint32_t e, int32_t t, int h) {
+  if (m.mf_steps > 0) {
+    if (t < 1 || t > m.mf_steps) return 0u;
+    return m.mf_tab[((size_t)e * (uint32_t)m.mf_steps + (uint32_t)(t - 1)) * (uint32_t)m.T + (uint32_t)h];
+  }
+  if (!(m.mf_rate > 0.0)) return 0u;
+  const uint64_t z = mf_draw(seed, (uint64_t)t, (uint64_t)h);
+  const double u = (double)(z >> 11) * (1.0 / 9007199254740992.0);
+  if (!(u < m.mf_rate)) return 0u;
+  return (uint32_t)(m.mf_min + (int32_t)(mix64(z ^ 0xA0761D6478BD642Full) % (uint64_t)(m.mf_max - m.mf_min + 1))) + 1u;
+}
 
 struct SflState {
   uint32_t E;
@@ -617,11 +634,7 @@ SFL_FN void env_tick(V& v) {
         }
       }
     }
-    if (st != S_DONE && mf == 0 && m.mf_rate > 0.0) {
-      uint64_t z = mf_draw(seed, (uint64_t)t, (uint64_t)h);
-      double u = (double)(z >> 11) * (1.0 / 9007199254740992.0);
-      if (u < m.mf_rate) mf = (uint32_t)(m.mf_min + (int32_t)(mix64(z ^ 0xA0761D6478BD642Full) % (uint64_t)(m.mf_max - m.mf_min + 1))) + 1u;
-    }
+    if (st != S_DONE && mf == 0) mf = mf_propose(m, seed, v.e, t, h);
     // preprocess_action
     uint32_t pa = given;
     if (pa == A_NOTHING && st == S_MOVING) pa = A_FWD;

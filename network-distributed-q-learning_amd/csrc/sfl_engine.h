@@ -14,6 +14,7 @@
 
 #include "../../include/sfl.h"
 #include "sfl_core.h"
+#include "sfl_mfgen.h"
 #include "sfl_part.h"
 
 namespace sfl {
@@ -410,6 +411,26 @@ int create(const sfl_map_desc* md, const sfl_hparams* hp, uint32_t n_envs, const
   }
   *out = h;
   return 0;
+}
+
+// Flatland-compatible malfunction stream: table[E][steps][T] proposals (sfl_mfgen.h); steps == 0
+// returns to the counter-based draw
+template <class B>
+int set_mf_schedule(Handle<B>* h, int32_t steps, const uint8_t* table) {
+  SflMap& m = h->map;
+  if (steps < 0 || (steps > 0 && !table)) return fail("sfl_set_mf_schedule: bad argument");
+  if (m.mf_tab) {
+    h->dfree((void*)m.mf_tab);
+    m.mf_tab = nullptr;
+  }
+  m.mf_steps = 0;
+  if (steps == 0) return 0;
+  const size_t n = (size_t)h->E * (size_t)steps * (size_t)m.T;
+  // (a byte is the train's malfunction counter field, tb_mf)
+  m.mf_tab = h->upload(table, n);
+  if (!m.mf_tab) return fail("sfl_set_mf_schedule: device allocation failed");
+  m.mf_steps = steps;
+  return h->be.sync() ? fail(h->be.error()) : 0;
 }
 
 // rng_states: [E][5] (state hi, state lo, inc hi, inc lo, has<<32|buf) — numpy's

@@ -903,12 +903,7 @@ struct WEnv {
             }
           }
         }
-        if (st_ != S_DONE && mf == 0 && m.mf_rate > 0.0) {
-          const uint64_t z = mf_draw(seed, (uint64_t)t, (uint64_t)h);
-          const double u = (double)(z >> 11) * (1.0 / 9007199254740992.0);
-          if (u < m.mf_rate)
-            mf = (uint32_t)(m.mf_min + (int32_t)(mix64(z ^ 0xA0761D6478BD642Full) % (uint64_t)(m.mf_max - m.mf_min + 1))) + 1u;
-        }
+        if (st_ != S_DONE && mf == 0) mf = mf_propose(m, seed, e, t, h);
         // preprocess_action
         uint32_t pa = given;
         if (pa == A_NOTHING && st_ == S_MOVING) pa = A_FWD;

@@ -40,7 +40,8 @@ class DistrQLearning:
         self.hp = dict(gamma=gamma, epsilon=epsilon, epsilon_decay_rate=epsilon_decay_rate, lr=lr,
                        lr_decay_rate=lr_decay_rate, default_q=default_q)
         seeds = [int(seed) + e for e in range(env.n_envs)]
-        self.batch = runtime.Batch(env.compiled, self.hp, seeds, lib=lib, device=env.device, max_steps=env.max_steps)
+        self.batch = runtime.Batch(env.compiled, self.hp, seeds, lib=lib, device=env.device, max_steps=env.max_steps,
+                                   malfunction_stream=getattr(env, "malfunction_stream", "counter"))
 
     # ------------------------------------------------------------------
     @property

@@ -11,7 +11,7 @@ from __future__ import annotations
 
 from typing import List, Optional, Sequence, Union
 
-from . import compiler, mapgen
+from . import compiler, mapgen, mfstream
 
 
 class Discrete:
@@ -32,10 +32,14 @@ class ASyncSwitchEnv:
 
     ``rail_env`` may be a ``mapgen.Scenario``, a config name from ``mapgen.CONFIGS`` or a
     path to a scenario JSON file (Flatland's RailEnv is not available in this build).
+    ``malfunction_stream="flatland"`` draws malfunctions in the order of Flatland's
+    ``ParamMalfunctionGen`` on the reset-seeded ``np_random`` (mfstream.py) instead of the
+    counter-based stream of the frozen spec.
     """
 
     def __init__(self, rail_env: Union[str, "mapgen.Scenario"], max_steps: int = 200, render_mode=None,
-                 observer=None, seed: Optional[int] = None, n_envs: int = 1, device: int = 0):
+                 observer=None, seed: Optional[int] = None, n_envs: int = 1, device: int = 0,
+                 malfunction_stream: str = "counter"):
         if observer is not None:
             raise NotImplementedError("custom observers are not supported on the device path")
         if isinstance(rail_env, str):
@@ -49,6 +53,7 @@ class ASyncSwitchEnv:
         self.seed = seed
         self.n_envs = int(n_envs)
         self.device = int(device)
+        self.malfunction_stream = mfstream.check_stream(malfunction_stream)
         cm = self.compiled
         self.possible_agents: List[str] = [f"switch_{r}-{c}" for r, c in cm.switch_ids]
         self.agents = self.possible_agents

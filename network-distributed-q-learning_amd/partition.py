@@ -80,10 +80,11 @@ class PartitionedBatch:
     def __init__(self, cm: CompiledMap, hp: dict, seeds: Sequence[int], env_base: int, envs_total: int,
                  rank: int = 0, world: int = 1, dist=None, lib: Optional[_lib.Lib] = None, device: int = 0,
                  owner: Optional[np.ndarray] = None, upd_per_env: int = 16, ntab: Optional[int] = None,
-                 buffer_device: str = "cuda", local_rows=True):
+                 buffer_device: str = "cuda", local_rows=True, malfunction_stream: str = "counter"):
         import torch
         self.torch = torch
         kw = {} if ntab is None else dict(ntab=ntab)
+        kw["malfunction_stream"] = malfunction_stream
         self.batch = Batch(cm, hp, seeds, lib=lib, device=device, **kw)
         self.lib = self.batch.lib
         self.cm, self.rank, self.world, self.dist = cm, int(rank), int(world), dist

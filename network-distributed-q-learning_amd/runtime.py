@@ -11,7 +11,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 
-from . import _lib
+from . import _lib, mfstream
 from .compiler import CompiledMap, eps_table, lr_table, NTAB
 
 P = C.POINTER
@@ -33,8 +33,11 @@ class Batch:
     """Owns one device handle.  ``hp`` uses the reference's DistrQLearning argument names."""
 
     def __init__(self, cm: CompiledMap, hp: dict, seeds: Sequence[int], lib: Optional[_lib.Lib] = None,
-                 device: int = 0, max_steps: int = 100_000, ntab: int = NTAB):
+                 device: int = 0, max_steps: int = 100_000, ntab: int = NTAB, malfunction_stream: str = "counter"):
+        """``malfunction_stream``: "counter" (the counter-based draw of the frozen Flatland spec,
+        oracle/flatland_lite.py) or "flatland" (ParamMalfunctionGen's np_random draw order, mfstream.py)."""
         self.cm = cm
+        self.malfunction_stream = mfstream.check_stream(malfunction_stream)
         self.hp = dict(hp)
         self.seeds = [int(s) for s in seeds]
         self.E = len(self.seeds)
@@ -92,6 +95,10 @@ class Batch:
                 self.close()
                 raise _lib.SflError(msg)
             warnings.warn(msg, RuntimeWarning, stacklevel=2)
+        if self.malfunction_stream == "flatland":
+            tab = mfstream.schedule(self.lib, sc, self.seeds)
+            self.lib.check(self.lib.dll.sfl_set_mf_schedule(self.h, tab.shape[1], _ptr(tab, C.c_uint8)),
+                           "sfl_set_mf_schedule")
         self.learn_calls = 0
         self.trace_env = None
         self.trace_cap = 1 << 16

@@ -104,6 +104,23 @@ def mf_draw(seed: int, tick: int, handle: int) -> int:
                  + (handle & M64) * 0x8CB92BA72F3D8DD7 + 0x632BE59BD9B4E019)
 
 
+def gym_seed_key(seed: int):
+    """``flatland.utils.seeding.np_random(seed)``'s argument to ``RandomState.seed`` (gym's seeding:
+    create_seed -> hash_seed (sha512 of str(seed), first 8 bytes) -> _int_list_from_bigint)."""
+    import hashlib
+    import struct
+    a = int(seed) % (1 << 64)
+    b = hashlib.sha512(str(a).encode("utf8")).digest()[:8] + b"\0" * 4
+    big = 0
+    for i, v in enumerate(struct.unpack("<3I", b)):
+        big += v << (32 * i)
+    ints = []
+    while big > 0:
+        big, mod = divmod(big, 1 << 32)
+        ints.append(mod)
+    return ints or [0]
+
+
 def mf_uniform(z: int) -> float:
     return (z >> 11) * (1.0 / 9007199254740992.0)
 
@@ -314,7 +331,15 @@ def motion_check(positions: List[Optional[Tuple[int, int]]], desired: List[Optio
 class RailEnv:
     """Speed-1 Flatland-semantics environment over a ``mapgen.Scenario``."""
 
-    def __init__(self, scenario, remove_agents_at_target: bool = True):
+    def __init__(self, scenario, remove_agents_at_target: bool = True, mf_stream: str = "counter"):
+        """``mf_stream``: "counter" (``mf_draw``) or "flatland": ParamMalfunctionGen's draws on the
+        env's ``np_random`` (numpy's RandomState, reseeded at every reset by a nonzero seed), for every
+        agent at every step in handle order -- ``rand() < 1 - exp(-rate)`` then ``randint(lo, hi + 1) + 1``
+        -- after the timetable's ``randint(0, departure_window_max)`` per agent at reset
+        (timetable_generators.py:113-115).  Parity with real Flatland unpinned (Flatland absent)."""
+        assert mf_stream in ("counter", "flatland")
+        self.mf_stream = mf_stream
+        self.np_random = None
         self.scenario = scenario
         self.rail = GridTransitionMap(scenario.grid)
         self.height, self.width = self.rail.height, self.rail.width
@@ -336,6 +361,13 @@ class RailEnv:
     def reset(self, regenerate_rail=True, regenerate_schedule=True, random_seed=None, **kw):
         self.random_seed = 0 if random_seed is None else int(random_seed)
         self._elapsed_steps = 0
+        if self.mf_stream == "flatland" and random_seed:
+            self.np_random = np.random.RandomState()
+            self.np_random.seed(gym_seed_key(self.random_seed))
+            mes = self._max_episode_steps
+            lam = mes - int(mes * 0.05)
+            for t in self.scenario.trains:  # the timetable generator's draws
+                self.np_random.randint(0, max(lam - (t.latest_arrival - t.earliest_departure), 1))
         # the same map + line every reset (the reference reseeds with a fixed seed: distr_q.py:195, 296)
         self.agents.sort(key=lambda a: a.handle)
         for h, a in enumerate(self.agents):
@@ -377,7 +409,16 @@ class RailEnv:
             h = a.handle
             a.old_position, a.old_direction = a.position, a.direction
             mh = a.malfunction_handler
-            if a.state != TrainState.DONE and mh.malfunction_down_counter == 0 and self.malfunction_rate > 0.0:
+            if self.mf_stream == "flatland":
+                if self.np_random is None:
+                    raise ValueError("the flatland malfunction stream needs reset(random_seed=<nonzero>)")
+                p = 1.0 - float(np.exp(-self.malfunction_rate)) if self.malfunction_rate > 0 else 0.0
+                n = 0
+                if self.np_random.rand() < p:
+                    n = int(self.np_random.randint(self.malfunction_min, self.malfunction_max + 1)) + 1
+                if a.state != TrainState.DONE and mh.malfunction_down_counter == 0 and n > 0:
+                    mh.malfunction_down_counter = n
+            elif a.state != TrainState.DONE and mh.malfunction_down_counter == 0 and self.malfunction_rate > 0.0:
                 z = mf_draw(self.random_seed, t, h)
                 if mf_uniform(z) < self.malfunction_rate:
                     mh.malfunction_down_counter = mf_duration(z, self.malfunction_min, self.malfunction_max) + 1

@@ -937,9 +937,9 @@ def sem_digest(semaphores) -> int:
     return zlib.crc32(repr(items).encode()) & 0xFFFFFFFF
 
 
-def build(scenario, seed, hp, max_steps=100_000, trace=True):
+def build(scenario, seed, hp, max_steps=100_000, trace=True, mf_stream="counter"):
     """Oracle (env, learner) for a ``mapgen.Scenario`` and reference-style hyper-parameters."""
-    rail_env = fl.RailEnv(scenario)
+    rail_env = fl.RailEnv(scenario, mf_stream=mf_stream)
     rail_env.reset()
     env = OracleEnv(rail_env, max_steps=max_steps)
     model = OracleDistrQ(env, gamma=hp["gamma"], epsilon=hp["epsilon"], epsilon_decay_rate=hp["epsilon_decay_rate"],

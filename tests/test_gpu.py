@@ -101,6 +101,31 @@ def test_c2_batch_gpu_equals_host_build_and_oracle(lib, kernel):
         assert bg.q_dict(e) == model.q
 
 
+@pytest.mark.parametrize("cfg,E", [("c2", 256), ("c3", 1024), ("c5", 8)])
+def test_flatland_malfunction_stream_gpu(lib, kernel, cfg, E):
+    """§8(f)4: the Flatland-compatible malfunction table (mfstream.py) read by the device kernels:
+    every env bit-equal to the host build, env 1 to the oracle drawing live from numpy's RandomState."""
+    from tests import hostsim
+    sc = mapgen.make_config(cfg, malfunction=(0.02, 5, 15))
+    cm = comp.compile_scenario(sc)
+    seeds = [777 + i for i in range(E)]
+    bg = runtime.Batch(cm, HP, seeds, lib=lib, ntab=1 << 14, malfunction_stream="flatland")
+    _check_kernel(bg, kernel)
+    bh = runtime.Batch(cm, HP, seeds, lib=hostsim.lib(), ntab=1 << 14, malfunction_stream="flatland")
+    og, oh = bg.learn(3), bh.learn(3)
+    for k in ("num_malfunctions", "cum_reward", "arrived", "decisions", "delays"):
+        assert np.array_equal(og[k], oh[k]), k
+    assert og["num_malfunctions"].sum() > 0
+    for e in range(E):
+        qg, tg = bg.q_raw(e)
+        qh, th = bh.q_raw(e)
+        assert np.array_equal(qg, qh) and np.array_equal(tg, th), f"env {e}"
+    env, model = so.build(sc, seeds[1], HP, trace=False, mf_stream="flatland")
+    ref = model.learn(3)
+    assert og["num_malfunctions"][:, 1].tolist() == ref["num_malfunctions"]
+    assert bg.q_dict(1) == model.q
+
+
 def test_c3_full_size_batch(lib):
     """BASELINE config: 64-switch / 32-train map, 65,536 envs on one GPU.  Size-independent
     checks on the whole batch + exact oracle parity on sampled envs."""
