@@ -77,6 +77,9 @@ typedef struct {
   const int32_t* tr_init_delay; /* [T] delay at reset */
   const uint8_t* tr_init_dir; /* [T] start heading */
   const int16_t* tr_init_port;/* [T] first switch port */
+  int32_t delay_threshold;    /* StandardObserver(delay_threshold=...) (observer.py:221, default 20): a train's
+                                 delay discretises to 1 while delay <= (latest_arrival - earliest_departure)
+                                 * delay_threshold (observer.py:228-244), else 2; |value| <= 65536 */
 } sfl_map_desc;
 
 typedef struct {

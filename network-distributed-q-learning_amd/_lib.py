@@ -30,7 +30,7 @@ class MapDesc(C.Structure):
         ("q_off", P(C.c_uint64)), ("row_base", P(C.c_uint32)), ("dist", P(C.c_int32)),
         ("tr_ed", P(C.c_int32)), ("tr_la", P(C.c_int32)), ("tr_k", P(C.c_int32)), ("tr_target", P(C.c_int32)),
         ("tr_init_cell", P(C.c_int32)), ("tr_init_dist", P(C.c_int32)), ("tr_init_delay", P(C.c_int32)),
-        ("tr_init_dir", P(C.c_uint8)), ("tr_init_port", P(C.c_int16)),
+        ("tr_init_dir", P(C.c_uint8)), ("tr_init_port", P(C.c_int16)), ("delay_threshold", C.c_int32),
     ]
 
 

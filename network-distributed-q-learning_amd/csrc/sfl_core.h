@@ -50,6 +50,7 @@ constexpr uint16_t PORT_NONE = 0xFFFFu;
 struct SflMap {
   int32_t H, W, S, T, K, NP, HW, cell_bits;  // cell_bits: bits of a cell index (HW - 1)
   int32_t max_episode_steps, mf_min, mf_max, ntab;
+  int32_t delay_thr;  // StandardObserver.delay_threshold (observer.py:221)
   double mf_rate, gamma, eps0, eps_decay, lr0, lr_decay, default_q;
   int64_t max_steps;
   uint64_t q_per_env;
@@ -949,7 +950,7 @@ SFL_FN void decide_observe(V& v, Obs& o, bool greedy) {
   const int32_t pos = v.pos(h);
   const int32_t delay = v.now - m.tr_la[h] + v.dist(h, pos, (int)tb_dir(b));
   const int32_t avail = m.tr_la[h] - m.tr_ed[h];
-  const uint32_t lvl = delay <= 0 ? 0u : (delay <= avail * 20 ? 1u : 2u);
+  const uint32_t lvl = delay <= 0 ? 0u : (delay <= (int64_t)avail * m.delay_thr ? 1u : 2u);
   const uint32_t state = ((free_bits * (uint32_t)m.K) + (uint32_t)m.tr_k[h]) * 3u + lvl;
   uint32_t amask = 1u << (na - 1);
   for (int a = 0; a < na - 1; ++a)

@@ -156,6 +156,7 @@ int create(const sfl_map_desc* md, const sfl_hparams* hp, uint32_t n_envs, const
   if (md->T > 32 * MAXW) return fail("sfl_create: at most 128 trains per env");
   if (md->S * 4 >= 0xFFFF) return fail("sfl_create: too many switches");
   if (md->K < 1 || md->K > 341) return fail("sfl_create: station count out of range");
+  if (md->delay_threshold < -65536 || md->delay_threshold > 65536) return fail("sfl_create: delay_threshold out of range");
   auto* h = new Handle<B>();
   h->device = device;
   if (int rc = h->be.init(device)) {
@@ -183,6 +184,7 @@ int create(const sfl_map_desc* md, const sfl_hparams* hp, uint32_t n_envs, const
   m.mf_rate = md->mf_rate;
   m.mf_min = md->mf_min;
   m.mf_max = md->mf_max;
+  m.delay_thr = md->delay_threshold;
   m.gamma = hp->gamma;
   m.eps0 = hp->epsilon;
   m.eps_decay = hp->epsilon_decay_rate;

@@ -1283,7 +1283,7 @@ struct WEnv {
     }
     const int32_t dl = now - la + dd;
     const int32_t avail = la - (int32_t)trw[0];
-    const uint32_t lvl = dl <= 0 ? 0u : (dl <= avail * 20 ? 1u : 2u);
+    const uint32_t lvl = dl <= 0 ? 0u : (dl <= avail * m.delay_thr ? 1u : 2u);
     const uint32_t state = ((fb * (uint32_t)m.K) + (uint32_t)k) * 3u + lvl;
     const uint32_t w = pr[1] >> 16, roff = pr[3] + state * w;
     const bool row_ok = pos_k >= 0 && dd < DIST_INF && (pin >> 2) == sw && slot < np;
@@ -1437,7 +1437,7 @@ struct WEnv {
     const int32_t d_obs = observe_only ? dist(k, p0, (int)tb_dir(b)) : dist_staged(d16_lo(U(pfd01[0])));
     const int32_t dl = now - la + d_obs;
     const int32_t avail = la - ed;
-    const uint32_t lvl = dl <= 0 ? 0u : (dl <= avail * 20 ? 1u : 2u);
+    const uint32_t lvl = dl <= 0 ? 0u : (dl <= avail * m.delay_thr ? 1u : 2u);
     const uint32_t state = ((free_bits * (uint32_t)m.K) + (uint32_t)k) * 3u + lvl;
     const uint32_t la7 = (uint32_t)lid() & 7u;
     const uint32_t srca = (swr.w[1] >> (2u * la7)) & 3u, dsta = (swr.w[1] >> (16u + 2u * la7)) & 3u;

@@ -41,7 +41,8 @@ class DistrQLearning:
                        lr_decay_rate=lr_decay_rate, default_q=default_q)
         seeds = [int(seed) + e for e in range(env.n_envs)]
         self.batch = runtime.Batch(env.compiled, self.hp, seeds, lib=lib, device=env.device, max_steps=env.max_steps,
-                                   malfunction_stream=getattr(env, "malfunction_stream", "counter"))
+                                   malfunction_stream=getattr(env, "malfunction_stream", "counter"),
+                                   delay_threshold=getattr(env, "delay_threshold", 20))
 
     # ------------------------------------------------------------------
     @property

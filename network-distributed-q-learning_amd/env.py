@@ -12,6 +12,7 @@ from __future__ import annotations
 from typing import List, Optional, Sequence, Union
 
 from . import compiler, mapgen, mfstream
+from . import observer as observer_mod
 
 
 class Discrete:
@@ -32,7 +33,8 @@ class ASyncSwitchEnv:
 
     ``rail_env`` may be a ``mapgen.Scenario``, a config name from ``mapgen.CONFIGS`` or a
     path to a scenario JSON file (Flatland's RailEnv is not available in this build).
-    ``malfunction_stream="flatland"`` draws malfunctions in the order of Flatland's
+    ``observer``: None or a ``StandardObserver`` (its ``delay_threshold`` reaches the kernels; see
+    observer.py).  ``malfunction_stream="flatland"`` draws malfunctions in the order of Flatland's
     ``ParamMalfunctionGen`` on the reset-seeded ``np_random`` (mfstream.py) instead of the
     counter-based stream of the frozen spec.
     """
@@ -40,8 +42,8 @@ class ASyncSwitchEnv:
     def __init__(self, rail_env: Union[str, "mapgen.Scenario"], max_steps: int = 200, render_mode=None,
                  observer=None, seed: Optional[int] = None, n_envs: int = 1, device: int = 0,
                  malfunction_stream: str = "counter"):
-        if observer is not None:
-            raise NotImplementedError("custom observers are not supported on the device path")
+        self.observer = observer
+        self.delay_threshold = observer_mod.delay_threshold_of(observer)
         if isinstance(rail_env, str):
             sc = mapgen.make_config(rail_env) if rail_env in mapgen.CONFIGS else mapgen.Scenario.load(rail_env)
         else:

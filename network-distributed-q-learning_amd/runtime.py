@@ -33,9 +33,11 @@ class Batch:
     """Owns one device handle.  ``hp`` uses the reference's DistrQLearning argument names."""
 
     def __init__(self, cm: CompiledMap, hp: dict, seeds: Sequence[int], lib: Optional[_lib.Lib] = None,
-                 device: int = 0, max_steps: int = 100_000, ntab: int = NTAB, malfunction_stream: str = "counter"):
+                 device: int = 0, max_steps: int = 100_000, ntab: int = NTAB, malfunction_stream: str = "counter",
+                 delay_threshold: int = 20):
         """``malfunction_stream``: "counter" (the counter-based draw of the frozen Flatland spec,
-        oracle/flatland_lite.py) or "flatland" (ParamMalfunctionGen's np_random draw order, mfstream.py)."""
+        oracle/flatland_lite.py) or "flatland" (ParamMalfunctionGen's np_random draw order, mfstream.py).
+        ``delay_threshold``: StandardObserver's (observer.py:221)."""
         self.cm = cm
         self.malfunction_stream = mfstream.check_stream(malfunction_stream)
         self.hp = dict(hp)
@@ -56,6 +58,7 @@ class Batch:
         md.max_episode_steps = sc.max_episode_steps
         md.mf_rate, md.mf_min, md.mf_max = sc.malfunction_rate, sc.malfunction_min, sc.malfunction_max
         md.q_per_env, md.rows_per_env = cm.q_per_env, cm.rows_per_env
+        md.delay_threshold = int(delay_threshold)
         spec = [("grid", np.uint16, C.c_uint16), ("cell_sw", np.int16, C.c_int16), ("sw_np", np.uint8, C.c_uint8),
                 ("sw_na", np.uint8, C.c_uint8), ("act_src", np.uint8, C.c_uint8), ("act_dst", np.uint8, C.c_uint8),
                 ("act_turn", np.uint8, C.c_uint8), ("act_j", np.uint8, C.c_uint8),

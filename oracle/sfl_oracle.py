@@ -937,11 +937,12 @@ def sem_digest(semaphores) -> int:
     return zlib.crc32(repr(items).encode()) & 0xFFFFFFFF
 
 
-def build(scenario, seed, hp, max_steps=100_000, trace=True, mf_stream="counter"):
+def build(scenario, seed, hp, max_steps=100_000, trace=True, mf_stream="counter", delay_threshold=20):
     """Oracle (env, learner) for a ``mapgen.Scenario`` and reference-style hyper-parameters."""
     rail_env = fl.RailEnv(scenario, mf_stream=mf_stream)
     rail_env.reset()
     env = OracleEnv(rail_env, max_steps=max_steps)
+    env.DELAY_THRESHOLD = delay_threshold  # StandardObserver(delay_threshold=...), observer.py:221
     model = OracleDistrQ(env, gamma=hp["gamma"], epsilon=hp["epsilon"], epsilon_decay_rate=hp["epsilon_decay_rate"],
                          lr=hp["lr"], lr_decay_rate=hp["lr_decay_rate"], default_q=hp["default_q"], seed=seed,
                          trace=trace)

@@ -126,6 +126,28 @@ def test_flatland_malfunction_stream_gpu(lib, kernel, cfg, E):
     assert bg.q_dict(1) == model.q
 
 
+@pytest.mark.parametrize("thr", [0, 1])
+def test_observer_delay_threshold_gpu(lib, kernel, thr):
+    """StandardObserver(delay_threshold=thr) (observer.py:221, 228-244) on the device: every env
+    bit-equal to the host build, env 3 to the oracle."""
+    from tests import hostsim
+    sc = mapgen.make_config("c2")
+    cm = comp.compile_scenario(sc)
+    seeds = [31 + i for i in range(128)]
+    bg = runtime.Batch(cm, HP, seeds, lib=lib, ntab=1 << 14, delay_threshold=thr)
+    _check_kernel(bg, kernel)
+    bh = runtime.Batch(cm, HP, seeds, lib=hostsim.lib(), ntab=1 << 14, delay_threshold=thr)
+    og, oh = bg.learn(3), bh.learn(3)
+    assert np.array_equal(og["cum_reward"], oh["cum_reward"])
+    for e in range(len(seeds)):
+        qg, tg = bg.q_raw(e)
+        qh, th = bh.q_raw(e)
+        assert np.array_equal(qg, qh) and np.array_equal(tg, th), f"env {e}"
+    env, model = so.build(sc, seeds[3], HP, trace=False, delay_threshold=thr)
+    model.learn(3)
+    assert bg.q_dict(3) == model.q
+
+
 def test_c3_full_size_batch(lib):
     """BASELINE config: 64-switch / 32-train map, 65,536 envs on one GPU.  Size-independent
     checks on the whole batch + exact oracle parity on sampled envs."""
