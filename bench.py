@@ -167,7 +167,10 @@ def main():
     mapgen = importlib.import_module(PKG + ".mapgen")
     comp = importlib.import_module(PKG + ".compiler")
     runtime = importlib.import_module(PKG + ".runtime")
-    importlib.import_module(PKG + ".build").build_hip()  # (re)build if the library is not from these sources
+    if rank == 0:  # (re)build if the library is not from these sources; the other ranks wait for it
+        importlib.import_module(PKG + ".build").build_hip()
+    if dist is not None:
+        dist.barrier()
     sc = mapgen.make_config(args.config)
     cm = comp.compile_scenario(sc)
     E = args.envs
@@ -258,7 +261,10 @@ def bench_partition(args):
     E = args.envs if args.envs != 65536 else 16384
     cm = comp.compile_scenario(mapgen.make_config(cfg))
     seeds = par.shard_seeds(450565, E, rank)
-    importlib.import_module(PKG + ".build").build_hip()
+    if rank == 0:
+        importlib.import_module(PKG + ".build").build_hip()
+    if dist is not None:
+        dist.barrier()
     local = not args.remote_rows
     if args.virtual_ranks > 1 and world == 1 and local:
         local = (part.partition_switches(cm, args.virtual_ranks) == 0).astype(np.uint8)
