@@ -2159,7 +2159,8 @@ __device__ void run_groups(const SflMap& m, const SflState& s, const SflCtl& c) 
 #ifdef SFL_PROFILE
   // group activity of the flat loop (per wave, lane 0): iterations, and per iteration the groups
   // that tick / post / decide, and the iterations with any tick
-  uint64_t gs[5] = {0, 0, 0, 0, 0};
+  uint64_t gs[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // + wall cycles of the tick / post / decide blocks
+  uint64_t tp0 = 0;
 #endif
   while (true) {
 #ifdef SFL_PROFILE
@@ -2198,6 +2199,9 @@ __device__ void run_groups(const SflMap& m, const SflState& s, const SflCtl& c) 
 #else
     const bool wave_decides = false;
 #endif
+#ifdef SFL_PROFILE
+    tp0 = __builtin_amdgcn_s_memtime();
+#endif
     if (phase == PH_TICK && !wave_decides) {
       abytes += 36u * (uint32_t)(m.T - mpopc(v.arr_mask));
       v.tick();
@@ -2205,6 +2209,13 @@ __device__ void run_groups(const SflMap& m, const SflState& s, const SflCtl& c) 
       if (v.flags & F_TERM) phase = (v.flags & F_INFLIGHT) ? PH_POST : PH_END;
       else if (many(v.q_mask)) phase = (v.flags & F_INFLIGHT) ? PH_POST : PH_DECIDE;
     }
+#ifdef SFL_PROFILE
+    {
+      const uint64_t t1 = __builtin_amdgcn_s_memtime();
+      gs[5] += t1 - tp0;
+      tp0 = t1;
+    }
+#endif
     if (phase == PH_POST) {  // post step + loop bookkeeping of the decision in flight
       const bool greedy = (v.flags & F_GREEDY) != 0;
       v.post(d, greedy);
@@ -2232,6 +2243,13 @@ __device__ void run_groups(const SflMap& m, const SflState& s, const SflCtl& c) 
       phase = (v.flags & (F_TERM | F_TRUNC)) ? PH_END : PH_DECIDE;
       if (dec_budget > 0 && (int64_t)v.n_dec >= dec_budget) break;
     }
+#ifdef SFL_PROFILE
+    {
+      const uint64_t t1 = __builtin_amdgcn_s_memtime();
+      gs[6] += t1 - tp0;
+      tp0 = t1;
+    }
+#endif
     if (phase == PH_DECIDE) {
       const bool greedy = (v.flags & F_GREEDY) != 0;
       v.decide(d, greedy);
@@ -2239,6 +2257,9 @@ __device__ void run_groups(const SflMap& m, const SflState& s, const SflCtl& c) 
       v.flags |= F_INFLIGHT;
       phase = many(v.q_mask) ? PH_POST : PH_TICK;
     }
+#ifdef SFL_PROFILE
+    gs[7] += __builtin_amdgcn_s_memtime() - tp0;
+#endif
     if (phase == PH_END) {
       const int arrived = mpopc(v.arr_mask);
       const size_t cap = (size_t)(c.stats_cap > 0 ? c.stats_cap : 1);
@@ -2278,10 +2299,14 @@ __device__ void run_groups(const SflMap& m, const SflState& s, const SflCtl& c) 
     uint64_t mx = gs[0];
     for (int off = 32; off > 0; off >>= 1) mx = max(mx, (uint64_t)__shfl_xor((long long)mx, off, 64));
     const int src = __builtin_ctzll(__ballot(gs[0] == mx));
-    uint64_t w[5];
-    for (int k = 0; k < 5; ++k) w[k] = (uint64_t)__shfl((long long)gs[k], src, 64);
+    uint64_t w[8];
+    for (int k = 0; k < 8; ++k) w[k] = (uint64_t)__shfl((long long)gs[k], src, 64);
     if (__lane_id() == 0)
-      for (int k = 0; k < 5; ++k) atomicAdd(&g_prof[k], (unsigned long long)w[k]);
+      for (int k = 0; k < 8; ++k) atomicAdd(&g_prof[k], (unsigned long long)w[k]);
+    if (v.lane == 0) {  // per group: decide's counters (prefetches, row / pending hits, decisions) and laps
+      for (int k = 3; k < 9; ++k) atomicAdd(&g_prof[5 + k], (unsigned long long)v.prof[k]);
+      for (int k = 0; k < 16; ++k) atomicAdd(&g_prof[16 + k], (unsigned long long)v.lap[k]);
+    }
   }
 #endif
   if (v.lane == 0) {
