@@ -40,11 +40,18 @@ __global__ void __launch_bounds__(SFL_WAVE_BLOCK) __attribute__((amdgpu_waves_pe
   sfl::wave::run<PPL, SPL, TW, TRACE>(*m, *s, *c);
 }
 // several envs per wavefront (sfl_wave.h run_groups): G lanes per env, SFL_WAVE_BLOCK / G envs per block
+// waves per SIMD the grouped kernel is register-budgeted for: shapes with one train slot per lane
+// (TW <= G) 4 -- c2 (variant 6): 918 M vs 805 M at 3 (VGPR-bound, spills a little; 5: 589 M) --,
+// two slots per lane 3 -- c3 (variant 7): the LDS allows 3 blocks per CU, and 128 VGPRs spill
+// (1,009 M vs 1,314 M)
+#ifndef SFL_GROUP_OCC1
+#define SFL_GROUP_OCC1 4
+#endif
 #ifndef SFL_GROUP_OCC
-#define SFL_GROUP_OCC 3  // waves per SIMD the grouped kernel is register-budgeted for (c3 at G = 16: LDS allows 3)
+#define SFL_GROUP_OCC 3
 #endif
 template <int PPL, int SPL, int TW, bool TRACE, int G>
-__global__ void __launch_bounds__(SFL_WAVE_BLOCK) __attribute__((amdgpu_waves_per_eu(SFL_GROUP_OCC)))
+__global__ void __launch_bounds__(SFL_WAVE_BLOCK) __attribute__((amdgpu_waves_per_eu(TW <= G ? SFL_GROUP_OCC1 : SFL_GROUP_OCC)))
 k_wave_g(const sfl::SflMap* __restrict__ m, const sfl::SflState* __restrict__ s, const sfl::SflCtl* __restrict__ c) {
   sfl::wave::run_groups<PPL, SPL, TW, TRACE, G>(*m, *s, *c);
 }
