@@ -1719,7 +1719,7 @@ struct WEnv {
   // env's update slots (k from the wave-uniform count n_upd)
   __device__ __forceinline__ void emit_upd(uint32_t k, int sw, int slot, uint32_t state, int j, uint32_t kind, double lr,
                                            double target, int stage) {
-    if (k >= P->upd_env) {
+    if (k >= P->upd_env || stage > 254) {  // (the record's stage field is 8 bits)
       lerr |= E_MSG_OVF;
       return;
     }
@@ -1827,8 +1827,9 @@ struct WEnv {
     SFL_LAP(10);
   }
   // PART: post with the Q operations on other ranks' rows as update records to their owners (env_post
-  // with MsgQ in sfl_part.h; stage stg = the pending update and key-set insert, stg + 1 + i = the
-  // bonus of the i-th arrived train), those on this rank's rows applied here as in post(); a
+  // with MsgQ in sfl_part.h; stage stg = the pending update and key-set insert, then one stage per
+  // arrived train's bonus -- only stages that carry records take a number), those on this rank's
+  // rows applied here as in post(); a
   // greedy decision's key-set insert on a remote row was done by its owner when it answered
   __device__ __forceinline__ void post_part(const Dec& d, bool greedy) {
     const bool loc_cur = local_sw(d.sw);
@@ -1851,7 +1852,6 @@ struct WEnv {
     const bool touch_rec = hp && d.sw != ps && !d.touch_cur && !loc_cur;
     const uint32_t k0 = n_upd;
     n_upd += (upd_rec ? 1u : 0u) + (touch_rec ? 1u : 0u);
-    if (stg > 254u) lerr |= E_MSG_OVF;
     if (lid() == 0) {
       if (hp) {
         if (loc_p) {
@@ -1876,10 +1876,13 @@ struct WEnv {
     Mask fresh = arr_mask & ~fl_mask;
     fl_mask |= fresh;
     if (many(fresh)) pf_ok = false;
-    uint32_t stage = stg + 1u;
+    // stages are numbered per launch and only those that carry records take a number: a launch
+    // that decides on local rows only (one rank: every row) emits none, however many posts it runs
+    uint32_t stage = stg + ((upd_rec || touch_rec) ? 1u : 0u);
     while (many(fresh)) {
       const int tr = mctz(fresh);
       mclear_low(fresh);
+      const uint32_t n_before = n_upd;
       for (int base = 0; base < m.S; base += G) {
         const int sw2 = base + lid();
         const bool valid = sw2 < m.S;
@@ -1910,7 +1913,7 @@ struct WEnv {
         }
         st(slotb, slot_ix(sw2, tr), slot_make(PEND_NONE, slot_rew(slw, epoch), epoch));
       }
-      ++stage;
+      if (n_upd != n_before) ++stage;
     }
     stg = stage;
     cset(d.sw, cget(d.sw) + 1u);
