@@ -48,7 +48,7 @@ __global__ void __launch_bounds__(SFL_WAVE_BLOCK) __attribute__((amdgpu_waves_pe
 #define SFL_GROUP_OCC1 4
 #endif
 #ifndef SFL_GROUP_OCC
-#define SFL_GROUP_OCC 3
+#define SFL_GROUP_OCC (SFL_PF_RING > 0 ? 4 : 3)  // two slots per lane: 4 with the prefetch ring (LDS 4 blocks/CU)
 #endif
 template <int PPL, int SPL, int TW, bool TRACE, int G>
 __global__ void __launch_bounds__(SFL_WAVE_BLOCK) __attribute__((amdgpu_waves_per_eu(TW <= G ? SFL_GROUP_OCC1 : SFL_GROUP_OCC)))

@@ -25,6 +25,12 @@
 namespace sfl {
 namespace wave {
 
+#ifndef SFL_PF_RING
+// grouped shapes with two train slots per lane: prefetch records per env (0: one per train).  A ring
+// of 10 fits four 16-env blocks per CU, but 4 waves per SIMD need <= 128 VGPRs (86 spilled): c3
+// 1,097 M vs 1,308 M; the ring alone at 3 waves 1,277 M.  Off by default
+#define SFL_PF_RING 0
+#endif
 #ifndef SFL_TICK_HOLD
 #define SFL_TICK_HOLD 2  // run_groups: ticks wait while this many groups of the wave can still decide
 #endif
@@ -260,9 +266,15 @@ struct WEnv {
   const int gbase;  // first wavefront lane of the group
   const SflPart* P;  // PART only
   static constexpr int TPL = (TWc + G - 1) / G;  // train slots per lane: trains lane, lane + G, ...
-  // prefetch records: one per queued train; PART stages only the train that decides in the launch
-  static constexpr int PF_SLOTS = PART ? 1 : TWc;
+  // prefetch records: one per queued train; PART stages only the train that decides in the launch.
+  // RING (grouped shapes with two train slots per lane, c3): PF_SLOTS records hold the first queued
+  // trains of a batch in queue order (record i = the i-th decision after the prefetch) and the
+  // batch is staged again when they are used up -- 360 instead of 1,152 bytes of LDS per env, so
+  // that four 16-env blocks fit a CU
+  static constexpr bool RING = !PART && G < 64 && TPL > 1 && SFL_PF_RING > 0 && SFL_PF_RING < TWc;
+  static constexpr int PF_SLOTS = PART ? 1 : (RING ? SFL_PF_RING : TWc);
   __device__ __forceinline__ static int pfx(int h) { return PART ? 0 : h; }
+  int pf_n = 0;  // RING: decisions since the batch was staged (= the record of the next one)
   static constexpr int kG = G;
   static_assert(TPL * G <= 128, "at most 128 train slots per env");
   using Mask = typename MaskOf<(TWc <= 32 ? 32 : TPL * G)>::type;
@@ -1175,10 +1187,16 @@ struct WEnv {
     // PART: a launch decides one train per env (the round ends at the next request, and the staging
     // does not survive the launch): stage that train only
     const int h_first = PART ? mctz(q_mask) : -1;
+    pf_n = 0;
 #pragma unroll 1
     for (int k = 0; k < TPL; ++k) {
       if (!mbit(q_mask, lid() + G * k)) continue;
       if (PART && lid() + G * k != h_first) continue;
+      if constexpr (RING) {  // a train beyond the records waits for the next staging
+        static_assert(sizeof(Mask) == 4, "RING: 32-bit train masks");
+        const uint32_t below = (uint32_t)q_mask & ((1u << (lid() + G * k)) - 1u);
+        if (__builtin_popcount(below) >= PF_SLOTS) continue;
+      }
       uint32_t roff, qoff;
       prefetch_slot(lid() + G * k, pick(sdec, k), pick(nprv, k), pick(bits, k), pick(pos, k), pick(plan, k), malf, greedy,
                     roff, qoff);
@@ -1212,8 +1230,10 @@ struct WEnv {
     const int slot = pin & 3;
     const int dir0 = (int)tb_dir(bits_k);
     const int pos0 = pos_k >= 0 ? pos_k : 0;
-    double* pfl = lpf + PF_D * pfx(hk);
-    uint32_t* pfi = lpi + PF_WI * pfx(hk);
+    int rec = pfx(hk);
+    if constexpr (RING) rec = __builtin_popcount((uint32_t)q_mask & ((1u << hk) - 1u));
+    double* pfl = lpf + PF_D * rec;
+    uint32_t* pfi = lpi + PF_WI * rec;
     // level 1: slot word, switch record, timetable row, the row block's port record, first moves
     const uint64_t slw = ld(slotb, slot_ix(sw, hk));
     const u4 w0 = sw_v4(sw, 0);
@@ -1377,7 +1397,7 @@ struct WEnv {
     // agent_iter: lowest queued train (switch_env.py:418-421, 616-622)
     // (PART observe pass: the observation needs one distance, looked up directly below; the
     // staging waits for the apply pass in the next launch)
-    if (!pf_ok && !observe_only) {
+    if ((!pf_ok || (RING && pf_n >= PF_SLOTS)) && !observe_only) {
       prefetch(greedy);
       pf_ok = !PART;  // (PART stages only this decision's train: the next one stages its own)
       SFL_PCNT(3);
@@ -1390,8 +1410,10 @@ struct WEnv {
     const int sw = (int)(sd >> 16);
     const SwRec swr = sw_rec(sw);
     const vec_t<int32_t, 8> tr = tr_row(h);
-    const double* pfh = lpf + PF_D * pfx(h);
-    const uint32_t* pfw = lpi + PF_WI * pfx(h);
+    const int rec = RING ? pf_n : pfx(h);
+    if constexpr (RING) pf_n += 1;
+    const double* pfh = lpf + PF_D * rec;
+    const uint32_t* pfw = lpi + PF_WI * rec;
     // the decision's LDS reads that do not depend on its observation, issued together: the staged
     // slot word (never stale: a decision writes only its own train's slots), row column, pending
     // cell value and distances, the epsilon-greedy stream and the switch's interaction count
@@ -2126,7 +2148,7 @@ __device__ void run_groups(const SflMap& m, const SflState& s, const SflCtl& c) 
   // per env: semaphores, counters, prefetch records, rng; per block: the timetable rows and the
   // per-switch / per-port map records (the groups of a wave read different switches' records: LDS
   // reads instead of vector loads)
-  constexpr int LDS_WORDS = (G * (PPL + SPL) + TW * PF_WORDS + 12 + 3) / 4 * 4;
+  constexpr int LDS_WORDS = (G * (PPL + SPL) + V::PF_SLOTS * PF_WORDS + 12 + 3) / 4 * 4;
   constexpr int EPB = SFL_WAVE_BLOCK / G;  // envs per block (sfl.hip launches)
   constexpr int SWX = G * SPL, NPX = G * PPL;  // switches / ports the shape holds
   constexpr int O_TT = EPB * LDS_WORDS, O_SW = O_TT + TW * 8, O_PP = O_SW + SWX * 16, O_PT = O_PP + NPX * 4;
