@@ -1543,11 +1543,7 @@ struct WEnv {
         uint32_t pick = 0;
         bool slow = nvalid > 1u;
         if (slow && m.seedseq32) {
-#ifdef SFL_X_NOSSQ  // timing only (results invalid): the table value replaced by the sub-seed itself
-          const uint64_t mm = (uint64_t)(U(sub_seed) * 2654435761u) * nvalid;
-#else
           const uint64_t mm = (uint64_t)LDC(m.seedseq32, (size_t)U(sub_seed)) * nvalid;
-#endif
           // Lemire rejects when the low word is below (2^32 - n) % n < n: test against n first
           slow = (uint32_t)mm < nvalid && (uint32_t)mm < (0u - nvalid) % nvalid;
           pick = (uint32_t)(mm >> 32);
