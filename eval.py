@@ -25,7 +25,8 @@ def evaluate(exp_dirs, model_file="distr_q_model.pkl", lib=None):
         print(f"Evaluating {exp_dir}")
         config = configparser.ConfigParser()
         config.read(os.path.join(exp_dir, "config.ini"))
-        env = ASyncSwitchEnv(build_scenario(config), render_mode="human", max_steps=100_000)
+        env = ASyncSwitchEnv(build_scenario(config), render_mode="human", max_steps=100_000,
+                             malfunction_stream=config["ENV"].get("malfunction_stream", "counter"))
         m = config["MODEL"]
         model = DistrQLearning(env=env, gamma=float(m["gamma"]), epsilon=float(m["epsilon"]),
                                epsilon_decay_rate=float(m["epsilon_decay_rate"]), lr=float(m["lr"]),

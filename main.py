@@ -4,7 +4,9 @@ Sections/keys as in the reference (main.py:21-60; writer hyperparam_tuning.py:49
   [MISC]  random_seed, out_dir, checkpoint_freq, exploit_freq   (+ optional n_envs, device)
   [ENV]   width, height, max_num_cities, max_rails_between_cities, max_rail_pairs_in_city,
           number_of_agents, malfunction_rate, min_duration, max_duration   (+ optional scenario:
-          a mapgen config name or a scenario JSON path, used instead of the size keys)
+          a mapgen config name or a scenario JSON path, used instead of the size keys; optional
+          malfunction_stream = counter | flatland: the frozen spec's counter-based draw, or
+          ParamMalfunctionGen's np_random draw order, mfstream.py)
 
 The size keys give mapgen's stand-in layout (mapgen.from_flatland_params), not Flatland's
 sparse_rail_generator output, which is absent: max_num_cities is honoured as a cap inside
@@ -49,7 +51,8 @@ def launch_experiment(config_path, lib=None):
     exploit_freq = int(config["MISC"]["exploit_freq"])
     n_envs = int(config["MISC"].get("n_envs", 1))
     device = int(config["MISC"].get("device", 0))
-    env = ASyncSwitchEnv(build_scenario(config), render_mode="human", max_steps=100_000, n_envs=n_envs, device=device)
+    env = ASyncSwitchEnv(build_scenario(config), render_mode="human", max_steps=100_000, n_envs=n_envs, device=device,
+                         malfunction_stream=config["ENV"].get("malfunction_stream", "counter"))
     m = config["MODEL"]
     model = DistrQLearning(env=env, gamma=float(m["gamma"]), epsilon=float(m["epsilon"]),
                            epsilon_decay_rate=float(m["epsilon_decay_rate"]), lr=float(m["lr"]),
