@@ -58,7 +58,7 @@ k_wave_g(const sfl::SflMap* __restrict__ m, const sfl::SflState* __restrict__ s,
 // maps with 65-128 trains (two train slots per lane): one env per 64-thread block (its LDS is
 // ~22 KB), register budget for the LDS-bound occupancy of 2 waves per SIMD
 #ifndef SFL_WAVE2_OCC
-#define SFL_WAVE2_OCC 2  // waves per SIMD k_wave2 is register-budgeted for
+#define SFL_WAVE2_OCC (SFL_PF_RING64 > 0 ? 4 : 2)  // waves per SIMD k_wave2 is register-budgeted for
 #endif
 template <int PPL, int SPL, int TW, bool TRACE>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SFL_WAVE2_OCC))) k_wave2(const sfl::SflMap* __restrict__ m,

@@ -31,6 +31,9 @@ namespace wave {
 // 1,097 M vs 1,308 M; the ring alone at 3 waves 1,277 M.  Off by default
 #define SFL_PF_RING 0
 #endif
+#ifndef SFL_PF_RING64
+#define SFL_PF_RING64 16  // one env per wavefront with two train slots per lane (c5, k_wave2): see WEnv::RING
+#endif
 #ifndef SFL_TICK_HOLD
 #define SFL_TICK_HOLD 2  // run_groups: ticks wait while this many groups of the wave can still decide
 #endif
@@ -267,12 +270,15 @@ struct WEnv {
   const SflPart* P;  // PART only
   static constexpr int TPL = (TWc + G - 1) / G;  // train slots per lane: trains lane, lane + G, ...
   // prefetch records: one per queued train; PART stages only the train that decides in the launch.
-  // RING (grouped shapes with two train slots per lane, c3): PF_SLOTS records hold the first queued
-  // trains of a batch in queue order (record i = the i-th decision after the prefetch) and the
-  // batch is staged again when they are used up -- 360 instead of 1,152 bytes of LDS per env, so
-  // that four 16-env blocks fit a CU
-  static constexpr bool RING = !PART && G < 64 && TPL > 1 && SFL_PF_RING > 0 && SFL_PF_RING < TWc;
-  static constexpr int PF_SLOTS = PART ? 1 : (RING ? SFL_PF_RING : TWc);
+  // RING (shapes with two train slots per lane): PF_SLOTS records hold the first queued trains of a
+  // batch in queue order (record i = the i-th decision after the prefetch) and the batch is staged
+  // again when they are used up.  c5 (k_wave2, one env per 64-thread block): 16 records instead of
+  // 128 take an env's LDS from 13.9 to 9.8 KB, so 16 envs fit a CU instead of 11, at 4 waves per
+  // SIMD in 128 VGPRs (1 spilled): 598 M -> 729 M agent-env-steps/s (ring of 32: 673 M).  c3 (G = 16):
+  // off by default, see SFL_PF_RING
+  static constexpr int RING_N = G < 64 ? SFL_PF_RING : SFL_PF_RING64;
+  static constexpr bool RING = !PART && TPL > 1 && RING_N > 0 && RING_N < TWc;
+  static constexpr int PF_SLOTS = PART ? 1 : (RING ? RING_N : TWc);
   __device__ __forceinline__ static int pfx(int h) { return PART ? 0 : h; }
   int pf_n = 0;  // RING: decisions since the batch was staged (= the record of the next one)
   static constexpr int kG = G;
@@ -1193,9 +1199,7 @@ struct WEnv {
       if (!mbit(q_mask, lid() + G * k)) continue;
       if (PART && lid() + G * k != h_first) continue;
       if constexpr (RING) {  // a train beyond the records waits for the next staging
-        static_assert(sizeof(Mask) == 4, "RING: 32-bit train masks");
-        const uint32_t below = (uint32_t)q_mask & ((1u << (lid() + G * k)) - 1u);
-        if (__builtin_popcount(below) >= PF_SLOTS) continue;
+        if (mpopc(q_mask & mbelow(Mask{}, lid() + G * k)) >= PF_SLOTS) continue;
       }
       uint32_t roff, qoff;
       prefetch_slot(lid() + G * k, pick(sdec, k), pick(nprv, k), pick(bits, k), pick(pos, k), pick(plan, k), malf, greedy,
@@ -1231,7 +1235,7 @@ struct WEnv {
     const int dir0 = (int)tb_dir(bits_k);
     const int pos0 = pos_k >= 0 ? pos_k : 0;
     int rec = pfx(hk);
-    if constexpr (RING) rec = __builtin_popcount((uint32_t)q_mask & ((1u << hk) - 1u));
+    if constexpr (RING) rec = mpopc(q_mask & mbelow(Mask{}, hk));
     double* pfl = lpf + PF_D * rec;
     uint32_t* pfi = lpi + PF_WI * rec;
     // level 1: slot word, switch record, timetable row, the row block's port record, first moves
@@ -1964,7 +1968,7 @@ template <int PPL, int SPL, int TW, bool TRACE, bool PART = false>
 __device__ void run(const SflMap& m, const SflState& s, const SflCtl& c, const SflPart* P = nullptr) {
   using V = WEnv<PPL, SPL, TW, PART>;
   // semaphores, counters, prefetch records, rng, timetable (PART: one record, timetable from the map)
-  constexpr int LDS_WORDS = 64 * (PPL + SPL) + (PART ? 1 : TW) * PF_WORDS + 12 + (PART ? 0 : TW * 8);
+  constexpr int LDS_WORDS = 64 * (PPL + SPL) + V::PF_SLOTS * PF_WORDS + 12 + (PART ? 0 : TW * 8);
   const int lane = (int)__lane_id();
   const uint32_t e = uni((uint32_t)((blockIdx.x * blockDim.x + threadIdx.x) >> 6));
   if (e >= s.E) return;
