@@ -42,8 +42,8 @@ __global__ void __launch_bounds__(SFL_WAVE_BLOCK) __attribute__((amdgpu_waves_pe
 // several envs per wavefront (sfl_wave.h run_groups): G lanes per env, SFL_WAVE_BLOCK / G envs per block
 // waves per SIMD the grouped kernel is register-budgeted for: shapes with one train slot per lane
 // (TW <= G) 4 -- c2 (variant 6): 918 M vs 805 M at 3 (VGPR-bound, spills a little; 5: 589 M) --,
-// two slots per lane 3 -- c3 (variant 7): the LDS allows 3 blocks per CU, and 128 VGPRs spill
-// (1,009 M vs 1,314 M)
+// two slots per lane 4 with the prefetch ring (SFL_PF_RING: the LDS then allows 4 blocks per CU),
+// 3 without it
 #ifndef SFL_GROUP_OCC1
 #define SFL_GROUP_OCC1 4
 #endif

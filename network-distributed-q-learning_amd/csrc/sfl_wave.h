@@ -27,9 +27,11 @@ namespace wave {
 
 #ifndef SFL_PF_RING
 // grouped shapes with two train slots per lane: prefetch records per env (0: one per train).  A ring
-// of 10 fits four 16-env blocks per CU, but 4 waves per SIMD need <= 128 VGPRs (86 spilled): c3
-// 1,097 M vs 1,308 M; the ring alone at 3 waves 1,277 M.  Off by default
-#define SFL_PF_RING 0
+// of 10 fits four 16-env blocks per CU (40.4 KB each), and 4 waves per SIMD then have to live in
+// 128 VGPRs: with the env's Q / key-set / slot base pointers held in registers 86 spilled (c3
+// 1,097 M vs 1,308 M at 3 waves); recomputed from the env index at each use (qbase / tbase /
+// sbase) 57, mostly in the episode-end bookkeeping: 1,351 M vs 1,298 M (3 waves, no ring)
+#define SFL_PF_RING 10
 #endif
 #ifndef SFL_PF_RING64
 #define SFL_PF_RING64 16  // one env per wavefront with two train slots per lane (c5, k_wave2): see WEnv::RING
@@ -672,11 +674,24 @@ struct WEnv {
   }
 
   // ---- Q-table ------------------------------------------------------------------------------
-  __device__ __forceinline__ double* qbase() const { return qb; }
+  // the env's global blocks; G < 64 recomputes them from e at each use (a held 64-bit pointer is
+  // two VGPRs per block for the whole loop)
+  __device__ __forceinline__ double* qbase() const {
+    if constexpr (PART || G == 64) return qb;
+    else return s.q + (size_t)e * m.q_per_env;
+  }
+  __device__ __forceinline__ uint32_t* tbase() const {
+    if constexpr (PART || G == 64) return touchb;
+    else return s.touched + (size_t)e * m.touched_words;
+  }
+  __device__ __forceinline__ uint64_t* sbase() const {
+    if constexpr (G == 64) return slotb;
+    else return s.slot + (size_t)e * (uint32_t)(m.S * m.T);
+  }
   // global-address-space atomic: a flat atomic would also count on lgkmcnt, so the decision's next
   // LDS read or scalar load would wait for its L2 round trip
   __device__ __forceinline__ void touch_row(uint32_t row) const {
-    __hip_atomic_fetch_or((SFL_AS_G uint32_t*)touchb + (row >> 5), 1u << (row & 31u), __ATOMIC_RELAXED,
+    __hip_atomic_fetch_or((SFL_AS_G uint32_t*)tbase() + (row >> 5), 1u << (row & 31u), __ATOMIC_RELAXED,
                           __HIP_MEMORY_SCOPE_AGENT);
   }
   // (a decaying lr past the table is an error, E_LR_TABLE: see SflEnv::lr_of in sfl_core.h)
@@ -847,7 +862,7 @@ struct WEnv {
     // new (switch, train) epoch: slots from older episodes read as empty
     epoch = (epoch + 1u) & 0xFFu;
     if (epoch == 0) {
-      for (int i = lane; i < m.S * m.T; i += G) st(slotb, (size_t)i, slot_make(PEND_NONE, 0, 0));
+      for (int i = lane; i < m.S * m.T; i += G) st(sbase(), (size_t)i, slot_make(PEND_NONE, 0, 0));
       epoch = 1;
     }
     cum = 0;
@@ -1239,7 +1254,7 @@ struct WEnv {
     double* pfl = lpf + PF_D * rec;
     uint32_t* pfi = lpi + PF_WI * rec;
     // level 1: slot word, switch record, timetable row, the row block's port record, first moves
-    const uint64_t slw = ld(slotb, slot_ix(sw, hk));
+    const uint64_t slw = ld(sbase(), slot_ix(sw, hk));
     const u4 w0 = sw_v4(sw, 0);
     const u4 w4 = sw_v4(sw, 1);  // compact-row descriptors
     const vec_t<uint32_t, 2> nbw = sw_nb_v(sw);
@@ -1776,7 +1791,7 @@ struct WEnv {
     if (greedy) {
       if (lid() == 0) {
         if (d.touch_cur) touch_row(d.row_cur);
-        st(slotb, slot_ix(d.next_sw, d.h), slot_make(PEND_NONE, d.r_new, epoch));
+        st(sbase(), slot_ix(d.next_sw, d.h), slot_make(PEND_NONE, d.r_new, epoch));
       }
       return;
     }
@@ -1813,8 +1828,8 @@ struct WEnv {
       if (d.touch_cur || (hp && d.sw != ps)) touch_row(d.row_cur);
 #endif
 #ifndef SFL_AB_NO_SLOT
-      st(slotb, slot_ix(d.sw, d.h), slot_make(PEND_NONE, slot_rew(d.slotword, epoch), epoch));
-      st(slotb, slot_ix(d.next_sw, d.h),
+      st(sbase(), slot_ix(d.sw, d.h), slot_make(PEND_NONE, slot_rew(d.slotword, epoch), epoch));
+      st(sbase(), slot_ix(d.next_sw, d.h),
          slot_make(pend_make((uint32_t)d.sw, (uint32_t)d.slot, d.state, (uint32_t)d.j), d.r_new, epoch));
 #endif
     }
@@ -1831,7 +1846,7 @@ struct WEnv {
       for (int base = 0; base < m.S; base += G) {
         const int sw2 = base + lid();
         const bool valid = sw2 < m.S;
-        const uint64_t slw = valid ? ld(slotb, slot_ix(sw2, tr)) : 0ull;
+        const uint64_t slw = valid ? ld(sbase(), slot_ix(sw2, tr)) : 0ull;
         const uint32_t pe = valid ? slot_pend(slw, epoch) : PEND_NONE;
         const int ps = pe == PEND_NONE ? 0 : (int)(pe & 0xFFFu);
         const uint32_t n = cget_var(ps);  // all lanes active: a bpermute reads 0 from inactive lanes
@@ -1846,7 +1861,7 @@ struct WEnv {
         const double b1 = lr * (1000.0 + m.gamma * 0.0);
         st(qp, 0, a1 + b1);
         touch_row(pr[2] + pstate);
-        st(slotb, slot_ix(sw2, tr), slot_make(PEND_NONE, slot_rew(slw, epoch), epoch));
+        st(sbase(), slot_ix(sw2, tr), slot_make(PEND_NONE, slot_rew(slw, epoch), epoch));
       }
     }
     cset(d.sw, cget(d.sw) + 1u);
@@ -1862,7 +1877,7 @@ struct WEnv {
     if (greedy) {
       if (lid() == 0) {
         if (loc_cur && d.touch_cur) touch_row(d.row_cur);
-        st(slotb, slot_ix(d.next_sw, d.h), slot_make(PEND_NONE, d.r_new, epoch));
+        st(sbase(), slot_ix(d.next_sw, d.h), slot_make(PEND_NONE, d.r_new, epoch));
       }
       return;
     }
@@ -1895,8 +1910,8 @@ struct WEnv {
       } else if (touch_rec) {
         emit_upd(k0 + (upd_rec ? 1u : 0u), d.sw, d.slot, d.state, 0, 1u, 0.0, 0.0, (int)stg);
       }
-      st(slotb, slot_ix(d.sw, d.h), slot_make(PEND_NONE, slot_rew(d.slotword, epoch), epoch));
-      st(slotb, slot_ix(d.next_sw, d.h),
+      st(sbase(), slot_ix(d.sw, d.h), slot_make(PEND_NONE, slot_rew(d.slotword, epoch), epoch));
+      st(sbase(), slot_ix(d.next_sw, d.h),
          slot_make(pend_make((uint32_t)d.sw, (uint32_t)d.slot, d.state, (uint32_t)d.j), d.r_new, epoch));
     }
     Mask fresh = arr_mask & ~fl_mask;
@@ -1912,7 +1927,7 @@ struct WEnv {
       for (int base = 0; base < m.S; base += G) {
         const int sw2 = base + lid();
         const bool valid = sw2 < m.S;
-        const uint64_t slw = valid ? ld(slotb, slot_ix(sw2, tr)) : 0ull;
+        const uint64_t slw = valid ? ld(sbase(), slot_ix(sw2, tr)) : 0ull;
         const uint32_t pe = valid ? slot_pend(slw, epoch) : PEND_NONE;
         const int ps2 = pe == PEND_NONE ? 0 : (int)(pe & 0xFFFu);
         const uint32_t n = cget_var(ps2);  // all lanes active: a bpermute reads 0 from inactive lanes
@@ -1937,7 +1952,7 @@ struct WEnv {
         } else {
           emit_upd(k, ps2, pslot, pstate, pj, 0u, lr_of_var(n), 1000.0 + m.gamma * 0.0, (int)stage);
         }
-        st(slotb, slot_ix(sw2, tr), slot_make(PEND_NONE, slot_rew(slw, epoch), epoch));
+        st(sbase(), slot_ix(sw2, tr), slot_make(PEND_NONE, slot_rew(slw, epoch), epoch));
       }
       if (n_upd != n_before) ++stage;
     }
