@@ -125,3 +125,16 @@ def test_partitioned_rounds_read_the_table():
         ref.step(n)
         assert pb.step(n) == n + 1
     _check_rank(pb, ref, range(4))
+
+
+def test_generator_rejects_bad_arguments():
+    lib = hostsim.lib()
+    k = np.array([1, 2], np.uint32)
+    w = np.array([5, 0], np.int32)
+    out = np.zeros((4, 2), np.uint8)
+    rc = lib.dll.sfl_mf_schedule_flatland(k.ctypes.data_as(P(C.c_uint32)), 2, w.ctypes.data_as(P(C.c_int32)), 2, 2,
+                                          0.5, 5, 15, 4, out.ctypes.data_as(P(C.c_uint8)))
+    assert rc != 0 and b"window" in lib.dll.sfl_last_error()
+    rc = lib.dll.sfl_mf_schedule_flatland(k.ctypes.data_as(P(C.c_uint32)), 2, None, 0, 2, 0.5, 9, 5, 4,
+                                          out.ctypes.data_as(P(C.c_uint8)))
+    assert rc != 0
