@@ -119,19 +119,69 @@ def dist_setup(par, local: int):
     return dist, dev, ("cuda" if backend == "nccl" else "cpu")
 
 
-def pmc_traffic(workload: str):
-    """HBM bytes per env-kernel launch from the committed rocprofv3 PMC summary of this exact kernel source
-    and workload (profiles/*_pmc.json written by scripts/pmc_summary.py), or None."""
+def pmc_profile(lib, workload: str):
+    """The committed rocprofv3 PMC summary (profiles/*_pmc.json, scripts/pmc_summary.py) of exactly this
+    library build (build id: sources + defines + flags) and workload, as (dict, path), or (None, None).
+    An experiment build never matches a product profile."""
     import glob
-    sha = importlib.import_module(PKG + ".build").kernel_source_sha1()
     for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc.json")), reverse=True):
         try:
             d = json.load(open(f))
         except Exception:
             continue
-        if d.get("source_sha1") == sha and d.get("workload") == workload:
-            return d["traffic_bytes_per_launch"], os.path.relpath(f, REPO)
+        if d.get("build_id", d.get("source_sha1")) == lib.build_id and d.get("workload") == workload:
+            return d, os.path.relpath(f, REPO)
     return None, None
+
+
+def library_info(lib):
+    return {"file": os.path.relpath(lib.path, REPO), "build_id": lib.build_id, "defines": lib.defines,
+            "experimental": bool(lib.experimental)}
+
+
+def issue_bound(prof):
+    """The binding bound of the env kernel from its PMC profile: the fraction of SIMD issue capacity its
+    vector instructions use (SQ_ACTIVE_INST_VALU quad-cycles over the SIMDs' wave-cycle budget), the
+    fraction of wave time spent waiting (SQ_WAIT_ANY / SQ_WAVE_CYCLES) and the VALU lane utilisation."""
+    if not prof:
+        return None
+    med = prof.get("per_launch_median", {})
+    out = {}
+    if "SQ_WAVE_CYCLES" in med and "SQ_WAIT_ANY" in med:
+        out["wait_frac"] = med["SQ_WAIT_ANY"] / med["SQ_WAVE_CYCLES"]
+    if "SQ_WAVE_CYCLES" in med and "SQ_ACTIVE_INST_ANY" in med:
+        out["active_frac"] = med["SQ_ACTIVE_INST_ANY"] / med["SQ_WAVE_CYCLES"]
+    if "SQ_THREAD_CYCLES_VALU" in med and "SQ_ACTIVE_INST_VALU" in med:
+        out["valu_lane_util"] = med["SQ_THREAD_CYCLES_VALU"] / (64.0 * med["SQ_ACTIVE_INST_VALU"])
+    for k in ("valu_issue_frac", "occupancy_waves_per_simd"):
+        if k in prof:
+            out[k] = prof[k]
+    return out or None
+
+
+def verify_fused(b, cm, seeds, schedule, n_envs: int):
+    """Parity of a spread sample of this rank's envs vs the host build of the kernel body (after timing)."""
+    build = importlib.import_module(PKG + ".build")
+    _lib = importlib.import_module(PKG + "._lib")
+    parity = importlib.import_module(PKG + ".parity")
+    host = _lib.Lib(build.build_hostsim())
+    host.check_fresh()
+    pick = parity.spread(len(seeds), n_envs)
+    bad = parity.check_batch(b, HP, pick, schedule, host)
+    return len(pick), bad
+
+
+def parity_field(dist, n_checked: int, bad, device=None):
+    """Job-wide parity verdict: envs checked and mismatches summed over ranks."""
+    par = importlib.import_module(PKG + ".parallel")
+    _, n_all = par.reduce_timing(dist, 0.0, float(n_checked), device=device)
+    _, nbad = par.reduce_timing(dist, 0.0, float(len(bad)), device=device)
+    return {"parity": "ok" if nbad == 0 and n_all > 0 else f"FAIL ({int(nbad)} mismatches)",
+            "parity_envs_checked": int(n_all),
+            "parity_reference": "libsfl_hostsim.so (the kernel body built for the host, pinned to the oracle and "
+                                "the reference's golden traces by tests/), same seeds and step schedule, "
+                                "Q-table + key set + env state bit-exact",
+            "parity_first_mismatches": list(bad[:4])}
 
 
 def main():
@@ -144,6 +194,11 @@ def main():
     ap.add_argument("--config", default="c3")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--verify-envs", type=int, default=8,
+                    help="envs per rank re-run on the host build after timing and compared bit-exactly (0: none)")
+    ap.add_argument("--experimental", action="store_true",
+                    help="accept a tuning / experiment build as SFL_LIB (its defines are reported; SFL_X_* / SFL_AB_* "
+                         "builds compute wrong results)")
     ap.add_argument("--remote-rows", action="store_true",
                     help="with --partition: every row operation travels as a message, also those on the rank's own "
                          "switches (the message path measured on one rank)")
@@ -155,6 +210,8 @@ def main():
                     help="graph-partitioned mode (BASELINE configs[4]): switch agents owned by ranks, RCCL all-to-all "
                          "of row lookups and updates; defaults to --config c5 --envs 16384 (238 GB of owned Q rows per GPU)")
     args = ap.parse_args()
+    if args.experimental:
+        os.environ["SFL_EXPERIMENTAL"] = "1"
     if args.partition:
         return bench_partition(args)
 
@@ -206,13 +263,19 @@ def main():
     barrier()
     dt = time.perf_counter() - t0
     dt, total_all = par.reduce_timing(dist, dt, float(total), device=red_dev)
+    # after the timed region: a spread sample of every rank's envs re-run on the host build, bit-exact
+    checked, bad = 0, ["not verified (--verify-envs 0)"]
+    if args.verify_envs > 0:
+        checked, bad = verify_fused(b, cm, seeds, [args.decisions] * (args.warmup + args.steps), args.verify_envs)
+    pfield = parity_field(dist, checked, bad, device=red_dev)
     if rank == 0:
         avg_ms = kms / max(1, args.steps)
         bytes_per_launch = abytes / max(1, args.steps)
         achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
         workload = (f"{args.config}: {cm.S} switches / {cm.T} trains, {E} envs per GPU, learning "
                     f"(eps-greedy + Q update), {args.decisions} agent-env-steps per env per step")
-        traffic, traffic_src = pmc_traffic(workload)
+        prof, prof_src = pmc_profile(b.lib, workload)
+        traffic = prof["traffic_bytes_per_launch"] if prof else None
         res = {
             "metric": METRIC,
             "value": total_all / dt,
@@ -231,10 +294,15 @@ def main():
                        "envs_per_gpu": E, "decisions_per_env_per_step": args.decisions,
                        "parallelism": f"env-batch dp{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": prof_src,
                          "kernel": kname, "avg_kernel_ms": avg_ms,
                          "alg_bytes_per_launch": bytes_per_launch,
-                         "ticks_per_decision": ticks_l / max(1, dec_l)},
+                         "ticks_per_decision": ticks_l / max(1, dec_l),
+                         "issue": issue_bound(prof)},
+            "library": library_info(b.lib),
+            "world_size": world,
+            "backend": (dist.get_backend() if dist is not None else None),
+            **pfield,
         }
         if world == 1 and not args.no_cpu:
             res["cpu_baseline"] = cpu_baseline(cm, args.cpu_seconds, args.config)
@@ -289,6 +357,20 @@ def bench_partition(args):
     dt = time.perf_counter() - t0
     total = float(E * args.decisions * args.steps)
     dt, total_all = par.reduce_timing(dist, dt, total, device=red_dev)
+    # after the timed region: a spread sample of the job's envs, this rank's owned rows of them and the
+    # state of those it simulates, vs a fused single-process host run of their seeds
+    checked, bad = 0, ["not verified (--verify-envs 0)"]
+    if args.verify_envs > 0:
+        build = importlib.import_module(PKG + ".build")
+        _lib = importlib.import_module(PKG + "._lib")
+        parity = importlib.import_module(PKG + ".parity")
+        host = _lib.Lib(build.build_hostsim())
+        host.check_fresh()
+        pick = parity.spread(world * E, args.verify_envs)
+        bad = parity.check_partition(pb, HP, pick, lambda g: 450565 + g, [args.decisions] * (args.warmup + args.steps),
+                                     host)
+        checked = len(pick)
+    pfield = parity_field(dist, checked, bad, device=red_dev)
     if rank == 0:
         res = {
             "metric": METRIC,
@@ -314,6 +396,10 @@ def bench_partition(args):
                        "envs_per_gpu": E, "decisions_per_env_per_step": args.decisions,
                        "rounds_per_step": rounds / max(1, args.steps),
                        "parallelism": f"env-batch dp{world} x switch-agent partition {world}"},
+            "library": library_info(pb.lib),
+            "world_size": world,
+            "backend": (dist.get_backend() if dist is not None else None),
+            **pfield,
         }
         print(json.dumps(res), flush=True)
     pb.close()

@@ -113,14 +113,28 @@ class Lib:
         if self.dll.sfl_abi_version() != ABI_VERSION:
             raise SflError("ABI version mismatch")
         self.build_id = self.dll.sfl_build_id().decode()
+        self.defines = ""
+        self.experimental = False
 
-    def check_fresh(self):
-        """Refuse a library built from other sources than the ones in this tree (a stale build)."""
+    def check_fresh(self, allow_experimental: bool = False):
+        """Refuse a library that is not the product build of the sources in this tree: a stale build, or a
+        tuning / experiment build (its -D defines or flags are part of its build id).  With
+        ``allow_experimental`` a build of these sources with the defines it records is accepted
+        (``self.defines`` then names them); experiment switches make its results invalid."""
         from . import build
-        want = build.kernel_source_sha1()
-        if self.build_id != want:
-            raise SflError(f"{self.path} is stale: built from sources {self.build_id[:12]}, the tree has {want[:12]} "
-                           f"(rebuild: python -c 'import __graft_entry__ as g; g.build()')")
+        want = build.product_build_id()
+        self.defines = build.built_defines(self.path) or ""
+        if self.build_id == want and not self.defines:
+            self.experimental = False
+            return
+        if allow_experimental and self.defines and self.build_id == build.build_id(self.defines.split()):
+            self.experimental = True
+            return
+        if self.defines:
+            raise SflError(f"{self.path} is a tuning / experiment build (defines: {self.defines}), not the product "
+                           f"library; set SFL_EXPERIMENTAL=1 (bench.py --experimental) to run it anyway")
+        raise SflError(f"{self.path} is stale: built as {self.build_id[:12]}, the tree's product build is {want[:12]} "
+                       f"(rebuild: python -c 'import __graft_entry__ as g; g.build()')")
 
     def check(self, rc: int, what: str):
         if rc != 0:
@@ -143,9 +157,10 @@ def load_product() -> Lib:
         # before libsfl.so resolves the same soname, so the library and torch's RCCL / allocator share it
         import torch  # noqa: F401
 
-        # SFL_LIB: an alternative in-tree build of the same HIP sources (tuning sweeps)
+        # SFL_LIB: an alternative in-tree build of the same HIP sources (tuning sweeps); accepted only with
+        # SFL_EXPERIMENTAL=1 unless it is the product build itself (check_fresh)
         lib = Lib(os.environ.get("SFL_LIB", PRODUCT_LIB))
-        lib.check_fresh()
+        lib.check_fresh(allow_experimental=os.environ.get("SFL_EXPERIMENTAL") == "1")
         if lib.device_count() < 1:
             raise SflError("libsfl.so loaded but no HIP device is visible: the SwitchFL hot path runs on MI355X only")
         _product = lib

@@ -21,6 +21,7 @@
 
 #include "sfl_core.h"
 #include "sfl_part.h"
+#include "sfl_experiment.h"
 
 namespace sfl {
 namespace wave {
@@ -876,10 +877,10 @@ struct WEnv {
   //      flatland_lite.RailEnv.step), train-parallel: lane h = train h ----------------------------
   __device__ __forceinline__ void tick() {
     SFL_LAP0();
-#ifdef SFL_X_NOTICK
-    ++now;
-    return;
-#endif
+    if constexpr (xp::kNoTick) {
+      ++now;
+      return;
+    }
     pf_ok = false;
     const int32_t t = ++now;
     const uint64_t seed = s.seed[e];
@@ -1238,10 +1239,10 @@ struct WEnv {
   __device__ __forceinline__ void prefetch_slot(const int hk, const uint32_t sdec_k, const uint32_t nprv_k,
                                                 const uint32_t bits_k, const int32_t pos_k, const uint32_t plan_k, Mask malf,
                                                 bool greedy, uint32_t& roff_out, uint32_t& qoff_out) {
-#ifdef SFL_X_NOPF
-    roff_out = qoff_out = PF_NONE;
-    return;
-#endif
+    if constexpr (xp::kNoPrefetch) {
+      roff_out = qoff_out = PF_NONE;
+      return;
+    }
     // Loads are issued by dependency level, unconditionally (clamped indices), so the chains
     // overlap: level 1 needs only this train's registers, level 2 the level-1 results, ...
     const int sw = (int)(sdec_k >> 16);
@@ -1441,11 +1442,9 @@ struct WEnv {
     const double pf_mx = pfh[2];
     const uint32_t pfd01[2] = {pfw[0], pfw[1]};
     const uint32_t pfd23[1] = {pfw[2]};
-#ifndef SFL_X_LATE_RNG
     uint64_t rng_w[5];
 #pragma unroll
     for (int i = 0; i < 5; ++i) rng_w[i] = lrng[i];
-#endif
     const uint32_t n_sw = cget(sw);
     const uint32_t pf_roff_h = trl(pf_roff, h), pf_qoff_h = trl(pf_qoff, h);
     const int np = swr.np();
@@ -1530,19 +1529,10 @@ struct WEnv {
     // epsilon-greedy
     int action = -1;
     bool explore = false;
-#ifdef SFL_X_NORNG
-    if (false) {
-#else
-    if (!greedy) {
-#endif
+    if (!greedy && !xp::kNoRng) {
       // (kept in VGPRs: the 128-bit LCG runs on the vector ALU's 64-bit multiply-adds; the scalar
       // unit is the contended one)
       Pcg64 rng;
-#ifdef SFL_X_LATE_RNG
-      uint64_t rng_w[5];
-#pragma unroll
-      for (int i = 0; i < 5; ++i) rng_w[i] = lrng[i];
-#endif
       rng.shi = rng_w[0];
       rng.slo = rng_w[1];
       rng.ihi = rng_w[2];
@@ -1551,7 +1541,8 @@ struct WEnv {
       rng.buf = (uint32_t)rng_w[4];
       const uint32_t n = n_sw;
       // eps0 * decay**n (distr_q.py:59-68): host-computed table (a scalar load, K$-resident), pow beyond it
-      const double eps = n < (uint32_t)m.ntab ? LDC(m.eps_tab, (size_t)n) : m.eps0 * pow_ool(m.eps_decay, (double)n);
+      const double eps = xp::kEpsConst ? m.eps0
+                         : n < (uint32_t)m.ntab ? LDC(m.eps_tab, (size_t)n) : m.eps0 * pow_ool(m.eps_decay, (double)n);
       explore = Ud(pcg_double(rng)) < eps;
       if (explore && !observe_only) {
         const uint32_t sub_seed = pcg_bounded(rng, 2147483646u);
@@ -1562,7 +1553,7 @@ struct WEnv {
         uint32_t pick = 0;
         bool slow = nvalid > 1u;
         if (slow && m.seedseq32) {
-          const uint64_t mm = (uint64_t)LDC(m.seedseq32, (size_t)U(sub_seed)) * nvalid;
+          const uint64_t mm = (uint64_t)(xp::kNoSeedSeqLoad ? (uint32_t)mix64(U(sub_seed)) : LDC(m.seedseq32, (size_t)U(sub_seed))) * nvalid;
           // Lemire rejects when the low word is below (2^32 - n) % n < n: test against n first
           slow = (uint32_t)mm < nvalid && (uint32_t)mm < (0u - nvalid) % nvalid;
           pick = (uint32_t)(mm >> 32);
@@ -1814,24 +1805,18 @@ struct WEnv {
       }
     }
     // every global write of the step from one lane-0 region
-    // (SFL_AB_*: timing-only tuning builds that drop one class of store, results invalid)
+    // (xp::kNo*: timing-only experiment builds that drop one class of store, sfl_experiment.h)
     if (lid() == 0) {
       if (hp) {
-#ifndef SFL_AB_NO_QST
-        st(qbase(), (size_t)d.qoff_pend, nv);
-#endif
-#ifndef SFL_AB_NO_TOUCH
-        touch_row(d.row_pend);
-#endif
+        if (!xp::kNoQStore) st(qbase(), (size_t)d.qoff_pend, nv);
+        if (!xp::kNoTouch) touch_row(d.row_pend);
       }
-#ifndef SFL_AB_NO_TOUCH
-      if (d.touch_cur || (hp && d.sw != ps)) touch_row(d.row_cur);
-#endif
-#ifndef SFL_AB_NO_SLOT
-      st(sbase(), slot_ix(d.sw, d.h), slot_make(PEND_NONE, slot_rew(d.slotword, epoch), epoch));
-      st(sbase(), slot_ix(d.next_sw, d.h),
-         slot_make(pend_make((uint32_t)d.sw, (uint32_t)d.slot, d.state, (uint32_t)d.j), d.r_new, epoch));
-#endif
+      if (!xp::kNoTouch && (d.touch_cur || (hp && d.sw != ps))) touch_row(d.row_cur);
+      if (!xp::kNoSlot) {
+        st(sbase(), slot_ix(d.sw, d.h), slot_make(PEND_NONE, slot_rew(d.slotword, epoch), epoch));
+        st(sbase(), slot_ix(d.next_sw, d.h),
+           slot_make(pend_make((uint32_t)d.sw, (uint32_t)d.slot, d.state, (uint32_t)d.j), d.r_new, epoch));
+      }
     }
     if (hp) pf_written(d.qoff_pend);
     // destination bonus for newly arrived trains (distr_q.py:344-356); lanes take switches.
@@ -1991,9 +1976,7 @@ __device__ void run(const SflMap& m, const SflState& s, const SflCtl& c, const S
   __shared__ uint32_t lds[WPB * LDS_WORDS];
   V v(m, s, e, lane, lds + (threadIdx.x >> 6) * LDS_WORDS, P);
   v.load();
-#ifdef SFL_AB_LOAD2
-  v.load();  // timing-only tuning build: the marginal cost of the state load
-#endif
+  if constexpr (xp::kLoadTwice) v.load();  // experiment build: the marginal cost of the state load
   const int64_t dec_base = PART ? (int64_t)uni((uint64_t)ld(P->dec_done, e)) : 0;
   int32_t phase = uni(ld(s.phase, e));
   int32_t ep_t = uni(ld(s.ep_t, e)), n_test = uni(ld(s.n_test, e));
@@ -2131,9 +2114,7 @@ __device__ void run(const SflMap& m, const SflState& s, const SflCtl& c, const S
     }
   }
   v.store(phase);
-#ifdef SFL_AB_STORE2
-  v.store(phase);  // timing-only tuning build: the marginal cost of the state store
-#endif
+  if constexpr (xp::kStoreTwice) v.store(phase);  // experiment build: the marginal cost of the state store
 #ifdef SFL_PROFILE
   prof[4] = (uint64_t)__builtin_amdgcn_s_memtime() - t_begin;
   if (lane == 0) {

@@ -214,6 +214,15 @@ class Batch:
         self.lib.check(self.lib.dll.sfl_get_q(self.h, env, _ptr(q, C.c_double), _ptr(t, C.c_uint32)), "sfl_get_q")
         return q, t
 
+    def set_q_raw(self, env: int, q: np.ndarray, touched: np.ndarray) -> None:
+        """Overwrite one env's compact Q block and key-set bitmap (the layout of q_raw)."""
+        q = np.ascontiguousarray(q, np.float64)
+        touched = np.ascontiguousarray(touched, np.uint32)
+        if q.size != self.cm.q_per_env or touched.size != (self.cm.rows_per_env + 31) // 32:
+            raise ValueError("set_q_raw: arrays do not match the map's Q layout")
+        self.lib.check(self.lib.dll.sfl_set_q(self.h, env, _ptr(q, C.c_double), _ptr(touched, C.c_uint32)),
+                       "sfl_set_q")
+
     def q_dict(self, env: int) -> Dict[tuple, list]:
         """Touched rows as {observation tuple: [Q per action]} — the reference's ``q_table``."""
         cm = self.cm

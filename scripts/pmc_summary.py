@@ -19,7 +19,7 @@ import sys
 def main(src, dst, bench_json=None):
     vals = {}
     kname = None
-    for d in sorted(glob.glob(os.path.join(src, "pmc_*"))):
+    for d in sorted(glob.glob(os.path.join(src, "pmc_*")) + glob.glob(os.path.join(src, "ws_*"))):
         for f in glob.glob(os.path.join(d, "*counter_collection.csv")):
             for r in csv.DictReader(open(f)):
                 if "k_run" in r["Kernel_Name"] or "k_wave" in r["Kernel_Name"]:
@@ -39,7 +39,13 @@ def main(src, dst, bench_json=None):
     if "SQ_WAVE_CYCLES" in med:
         out["wait_fraction"] = med.get("SQ_WAIT_ANY", 0) / med["SQ_WAVE_CYCLES"]
     if bench_json:
-        out["workload"] = json.load(open(bench_json))["config"]["workload"]
+        bj = json.load(open(bench_json))
+        out["workload"] = bj["config"]["workload"]
+        # the build id of the library the passes ran (sources + defines + flags): bench.py attaches this
+        # profile only to a run of exactly that build
+        if "library" in bj:
+            out["build_id"] = bj["library"]["build_id"]
+            out["defines"] = bj["library"]["defines"]
     json.dump(out, open(dst, "w"), indent=1)
     print(json.dumps(out, indent=1))
 

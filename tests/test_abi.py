@@ -112,3 +112,55 @@ def test_handle_argument_errors():
     b.apply_qinit()
     assert b.step(8)[0] == 16
     b.close()
+
+
+# ---- build provenance (round 3): the build id covers the defines and flags ------------------------
+def test_build_id_covers_defines():
+    assert build.build_id() == build.kernel_source_sha1() == build.product_build_id()
+    a, b = build.build_id(["SFL_TICK_HOLD=1"]), build.build_id(["SFL_TICK_HOLD=2"])
+    assert len({a, b, build.build_id()}) == 3
+    assert build.build_id(flags=["-O2"]) != build.build_id()
+    assert build.build_id(["B", "A"]) == build.build_id(["A", "B"])
+
+
+def test_product_library_carries_no_defines():
+    path = build.build_hip()
+    assert build.built_id(path) == build.product_build_id()
+    assert build.built_defines(path) == ""
+    lib = _lib.Lib(path)
+    lib.check_fresh()
+    assert lib.defines == "" and not lib.experimental
+
+
+def test_defines_are_refused_into_the_product_path():
+    with pytest.raises(ValueError, match="product"):
+        build.build_hip(defines=["SFL_X_NOTICK"])
+    with pytest.raises(ValueError, match="product"):
+        build.build_hip(flags=["-O1"])
+    with pytest.raises(ValueError):
+        build.build_hostsim(defines=["SFL_TICK_HOLD=1"])
+
+
+def test_define_built_library_fails_check_fresh(tmp_path):
+    """A library built with a -D define is not the product build: check_fresh refuses it (bench.py and
+    every product entry point load through it), and accepts it only when experiments are allowed,
+    naming its defines."""
+    path = build.build_hostsim(out_dir=str(tmp_path), defines=["SFL_TICK_HOLD=3"])
+    assert build.built_defines(path) == "SFL_TICK_HOLD=3"
+    lib = _lib.Lib(path)
+    with pytest.raises(_lib.SflError, match="experiment"):
+        lib.check_fresh()
+    lib.check_fresh(allow_experimental=True)
+    assert lib.experimental and lib.defines == "SFL_TICK_HOLD=3"
+
+
+def test_experiment_switch_needs_the_experiment_build():
+    """The timing-only switches that make results invalid compile only together with SFL_EXPERIMENT,
+    which build_hip adds itself (and refuses into libsfl.so)."""
+    import subprocess
+    hdr = os.path.join(REPO, "network-distributed-q-learning_amd", "csrc", "sfl_experiment.h")
+    r = subprocess.run(["g++", "-std=c++17", "-fsyntax-only", "-x", "c++", "-DSFL_X_NOTICK", hdr], capture_output=True)
+    assert r.returncode != 0 and b"SFL_EXPERIMENT" in r.stderr
+    r = subprocess.run(["g++", "-std=c++17", "-fsyntax-only", "-x", "c++", "-DSFL_X_NOTICK", "-DSFL_EXPERIMENT", hdr],
+                       capture_output=True)
+    assert r.returncode == 0, r.stderr
