@@ -25,6 +25,12 @@
  *                     (learning mode, episodes restart as they end; the benchmark step)
  *   sfl_get_q / sfl_set_q   DistrQLearning.q_table / save / load     switchfl/distr_q.py:492-527
  *   sfl_get_counters  timing/progress accumulators                   switchfl/switch_env.py:67-73
+ *   sfl_env_begin / sfl_env_step   the AEC protocol with an external learner:
+ *                     env.reset / agent_iter / last / step(action) / observe
+ *                                                                    switchfl/switch_env.py:93, 616-675
+ *                     (driven by any learner, e.g. distr_q.py:302-320)
+ *   sfl_get_phase_cycles   the per-phase time accumulators            switchfl/switch_env.py:67-73
+ *                     (flatland_step_time, last_time, action_selection_time, update_time, reset_time ...)
  */
 #ifndef SFL_H
 #define SFL_H
@@ -35,7 +41,7 @@
 extern "C" {
 #endif
 
-#define SFL_ABI_VERSION 6
+#define SFL_ABI_VERSION 7
 
 typedef struct sfl_handle sfl_handle;
 
@@ -206,6 +212,42 @@ int sfl_part_set_local_rows(sfl_handle* h, const uint8_t* local_switches);
  * (other entries untouched); owned key-set bits OR-ed into touched */
 int sfl_part_get_q(sfl_handle* h, uint32_t global_env, double* q, uint32_t* touched);
 
+/* ---- external-action mode: the AEC protocol with the policy / learner on the host ----
+ * sfl_env_begin turns the handle into n_envs plain environments (no learner: no epsilon draw, no Q-table
+ * access), each at a fresh reset.  Each sfl_env_step call then, per env: applies actions[e] to the
+ * observation the previous call emitted (ASyncSwitchEnv.step -> _apply_action, and _move_trains_to_switch
+ * when no switch is active: switch_env.py:632-666), and runs on to the env's next decision, whose
+ * observation it emits (agent_iter pops it, last() / observe() read it: switch_env.py:616-630, 668-675,
+ * observer.py:246-308) -- or reports the episode's end (agent = -1; the next call resets:
+ * switch_env.py:93-158).  actions == null (or an action < 0) applies nothing and re-emits the pending
+ * observation.  Output arrays are host pointers, [n_envs] unless stated; null skips one. */
+typedef struct {
+  const int32_t* actions;  /* in: action for each env's pending observation (< 0 or null: none) */
+  int32_t* agent;          /* deciding switch index of the emitted observation; -1: the episode ended */
+  int32_t* train;          /* active train (info["active_train"]) */
+  int32_t* slot;           /* in-port slot of the active train at the switch */
+  uint32_t* state;         /* observation index ((free_port_bits * K + station) * 3 + delay level): the
+                              observation vector [r, c, sem[P], target[2P], delay[P]] (observer.py:269-308) */
+  uint32_t* mask;          /* info["action_mask"] as bits (bit a: action a allowed) */
+  int32_t* reward;         /* last() reward of (agent, train) (switch_env.py:289, AECEnv.last) */
+  int32_t* now;            /* rail_env._elapsed_steps at the observation */
+  int32_t* next_switch;    /* step() "next_switch" of the applied action (-1: none applied) */
+  int32_t* step_now;       /* _elapsed_steps when that step() returned (-1: none applied) */
+  uint32_t* arrived;       /* [4][n_envs] arrived-train bitmask ("arrived_trains") after this call */
+  int32_t* malfunctions;   /* episode end: num_malfunctions */
+  int32_t* delays;         /* episode end: [T][n_envs] train_to_last_node delays */
+  int32_t* truncated;      /* episode end: 1 truncation (max_steps), 0 termination */
+} sfl_env_io;
+int sfl_env_begin(sfl_handle* h);
+int sfl_env_step(sfl_handle* h, sfl_env_io* io);
+/* Device time per phase of the learn loop since create, accumulated from in-kernel cycle counters of a
+ * sample of the wavefronts (the kernels with one env per lane group; zero for the lane-per-env body):
+ * cycles[0] tick (Flatland RailEnv.step + _move_trains / _check_active_switch), [1] observe (last()),
+ * [2] epsilon-greedy action selection, [3] apply (_apply_action), [4] post (Q update, pending map,
+ * destination bonus), [5] reset, [6] other (launch state load / store, loop control), [7] the sampled
+ * wavefronts' total; their ratios split the launches' kernel time (switch_env.py:67-73 accumulators).
+ * n >= 8. */
+int sfl_get_phase_cycles(sfl_handle* h, uint64_t* cycles, int32_t n);
 #ifdef __cplusplus
 }
 #endif

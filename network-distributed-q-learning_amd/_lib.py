@@ -12,7 +12,7 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 PRODUCT_LIB = os.path.join(HERE, "libsfl.so")
-ABI_VERSION = 6  # include/sfl.h SFL_ABI_VERSION
+ABI_VERSION = 7  # include/sfl.h SFL_ABI_VERSION
 
 P = C.POINTER
 
@@ -58,6 +58,14 @@ class Counters(C.Structure):
                 ("last_kernel_ms", C.c_double), ("kernel_variant", C.c_int32), ("group_lanes", C.c_int32)]
 
 
+class EnvIO(C.Structure):
+    """sfl_env_io (external-action mode)."""
+    _fields_ = [("actions", P(C.c_int32)), ("agent", P(C.c_int32)), ("train", P(C.c_int32)), ("slot", P(C.c_int32)),
+                ("state", P(C.c_uint32)), ("mask", P(C.c_uint32)), ("reward", P(C.c_int32)), ("now", P(C.c_int32)),
+                ("next_switch", P(C.c_int32)), ("step_now", P(C.c_int32)), ("arrived", P(C.c_uint32)),
+                ("malfunctions", P(C.c_int32)), ("delays", P(C.c_int32)), ("truncated", P(C.c_int32))]
+
+
 EXPORTS = {
     "sfl_abi_version": (C.c_int, []),
     "sfl_build_id": (C.c_char_p, []),
@@ -75,6 +83,10 @@ EXPORTS = {
     "sfl_set_q": (C.c_int, [C.c_void_p, C.c_uint32, P(C.c_double), P(C.c_uint32)]),
     "sfl_get_counters": (C.c_int, [C.c_void_p, P(Counters)]),
     "sfl_get_kernel_note": (C.c_int, [C.c_void_p, C.c_char_p, C.c_int32]),
+    # external-action mode (aec.py) and the per-phase device time (distr_q.py timing accumulators)
+    "sfl_env_begin": (C.c_int, [C.c_void_p]),
+    "sfl_env_step": (C.c_int, [C.c_void_p, P(EnvIO)]),
+    "sfl_get_phase_cycles": (C.c_int, [C.c_void_p, P(C.c_uint64), C.c_int32]),
     "sfl_get_env_state": (C.c_int, [C.c_void_p, C.c_uint32, P(C.c_int32), P(C.c_int32), P(C.c_uint64),
                                     P(C.c_int32), P(C.c_uint32)]),
     # Flatland-compatible malfunction stream (mfstream.py)
@@ -130,6 +142,9 @@ class Lib:
         if allow_experimental and self.defines and self.build_id == build.build_id(self.defines.split()):
             self.experimental = True
             return
+        if self.defines and allow_experimental:
+            raise SflError(f"{self.path} is stale: a tuning / experiment build (defines: {self.defines}) of other "
+                           f"sources than the tree's (rebuild it)")
         if self.defines:
             raise SflError(f"{self.path} is a tuning / experiment build (defines: {self.defines}), not the product "
                            f"library; set SFL_EXPERIMENTAL=1 (bench.py --experimental) to run it anyway")

@@ -32,6 +32,14 @@ __global__ void __launch_bounds__(256) k_run(const sfl::SflMap* __restrict__ m, 
   if (e < s->E) sfl::env_run<NW>(*m, *s, *c, e);
 }
 
+// external-action mode (sfl_env_step): the lane-per-env body without the learner, one decision per call
+template <int NW>
+__global__ void __launch_bounds__(256) k_run_ext(const sfl::SflMap* __restrict__ m, const sfl::SflState* __restrict__ s,
+                                                 const sfl::SflCtl* __restrict__ c) {
+  const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < s->E) sfl::env_run_ext<NW>(*m, *s, *c, e);
+}
+
 // One env per wavefront (sfl_wave.h): 4 envs per block.  PPL / SPL = semaphore / counter
 // registers per lane (sfl::kVariants).
 template <int PPL, int SPL, int TW, bool TRACE>
@@ -482,6 +490,37 @@ struct HipBackend {
 #ifdef SFL_PROFILE
     if (variant > 0) print_prof();
 #endif
+    return err.empty() ? 0 : -1;
+  }
+  // external-action mode: one call = every env applies its action and runs to its next observation
+  int run_ext(const sfl::SflMap& m, const sfl::SflState& s, const sfl::SflCtl& c, float* ms) {
+    struct {
+      sfl::SflMap m;
+      char p0[(sizeof(sfl::SflMap) + 63) / 64 * 64 - sizeof(sfl::SflMap)];
+      sfl::SflState s;
+      char p1[(sizeof(sfl::SflState) + 63) / 64 * 64 - sizeof(sfl::SflState)];
+      sfl::SflCtl c;
+    } hp;
+    hp.m = m;
+    hp.s = s;
+    hp.c = c;
+    const size_t os = (sizeof(sfl::SflMap) + 63) / 64 * 64, oc = os + (sizeof(sfl::SflState) + 63) / 64 * 64;
+    char* base = (char*)d_params;
+    check(hipMemcpyAsync(d_params, &hp, sizeof(hp), hipMemcpyHostToDevice, stream), "params h2d");
+    check(hipEventRecord(ev0, stream), "event");
+    const auto* pm = (const sfl::SflMap*)base;
+    const auto* ps = (const sfl::SflState*)(base + os);
+    const auto* pc = (const sfl::SflCtl*)(base + oc);
+    const unsigned blocks = (s.E + 63) / 64;  // (64-thread blocks: few envs, spread over the CUs)
+    if (m.T <= 32) k_run_ext<1><<<blocks, 64, 0, stream>>>(pm, ps, pc);
+    else if (m.T <= 64) k_run_ext<2><<<blocks, 64, 0, stream>>>(pm, ps, pc);
+    else k_run_ext<4><<<blocks, 64, 0, stream>>>(pm, ps, pc);
+    if (!check(hipGetLastError(), "k_run_ext launch")) return -1;
+    check(hipEventRecord(ev1, stream), "event");
+    if (!check(hipEventSynchronize(ev1), "k_run_ext")) return -1;
+    float t = 0.f;
+    hipEventElapsedTime(&t, ev0, ev1);
+    *ms = t;
     return err.empty() ? 0 : -1;
   }
   int sync() { return check(hipStreamSynchronize(stream), "sync") && err.empty() ? 0 : -1; }

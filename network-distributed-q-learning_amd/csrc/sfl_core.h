@@ -31,6 +31,9 @@ enum : uint32_t { A_NOTHING = 0, A_LEFT = 1, A_FWD = 2, A_RIGHT = 3, A_STOP = 4,
 enum : uint32_t { S_WAITING = 0, S_READY = 1, S_MF_OFF = 2, S_MOVING = 3, S_STOPPED = 4, S_MALF = 5, S_DONE = 6 };
 enum : int32_t { PH_RESET = 0, PH_TICK = 1, PH_DECIDE = 2, PH_POST = 3, PH_END = 4 };
 enum : uint32_t { F_TERM = 1, F_TRUNC = 2, F_GREEDY = 4, F_EXPLOIT_DONE = 8, F_OWN_SCAN = 16, F_INFLIGHT = 32 };
+// (64: F_REQ, sfl_part.h; 128: F_EXT_OBS, an observation was emitted in external-action mode and its
+// action is due)
+enum : uint32_t { F_EXT_OBS = 128 };
 enum : uint32_t {
   E_INF_DIST = 1,      // observer.py:35-36 would raise ValueError
   E_PLAN_OVF = 2,      // train plan longer than the packed ring
@@ -175,6 +178,30 @@ struct SflCtl {
   uint64_t* trace_n;     // records written
   int32_t trace_env;
   int32_t trace_cap;
+  const struct SflExt* ext;  // external-action mode (mode 2) buffers, device memory; null otherwise
+};
+
+// External-action mode (sfl_env_step): the env alone, stepped one decision per call by a policy on the
+// host -- the PettingZoo AEC protocol agent_iter / last / step(action) / observe (switch_env.py:616-675)
+// driven by any learner (distr_q.py:302-320).  Per env and call: the action for the observation the
+// previous call emitted is applied (_apply_action, then the Flatland ticks up to the next decision if
+// no switch is active), and the env runs on to its next decision, whose observation is emitted; an
+// episode end is reported instead (agent = -1) and the next call starts the next episode.
+struct SflExt {
+  const int32_t* actions;  // [E] in: action for the pending observation (< 0: none)
+  int32_t* agent;          // [E] deciding switch (-1: the episode ended in this call)
+  int32_t* train;          // [E] active train
+  int32_t* slot;           // [E] in-port slot of the active train at the switch
+  uint32_t* state;         // [E] observation index ((free_bits * K + k) * 3 + delay level)
+  uint32_t* mask;          // [E] action mask bits
+  int32_t* reward;         // [E] AECEnv.last() reward of (switch, train)
+  int32_t* now;            // [E] elapsed ticks at the observation
+  int32_t* next_sw;        // [E] successor switch of the applied action (-1: none applied)
+  int32_t* step_now;       // [E] elapsed ticks when the applied action's step() returned
+  uint32_t* arrived;       // [MAXW][E] arrived trains (bitmask) after the step / at the episode end
+  int32_t* n_mf;           // [E] malfunctions counted in the episode
+  int32_t* delays;         // [T][E] train_to_last_node delays at the episode end
+  int32_t* truncated;      // [E] the episode ended by max_steps truncation (1) or termination (0)
 };
 
 // ---------------------------------------------------------------------------
@@ -1313,6 +1340,103 @@ SFL_FN void env_run(const SflMap& m, const SflState& s, const SflCtl& c, uint32_
   if (c.launch_dec) c.launch_dec[e] = dec;
   if (c.launch_ticks) c.launch_ticks[e] = ticks;
   if (c.launch_bytes) c.launch_bytes[e] = abytes;
+}
+
+// ---------------------------------------------------------------------------
+// external-action mode (SflExt): one env, one decision per call, the action from the host
+// ---------------------------------------------------------------------------
+// The env's operations are env_run's in the same order (reset, ticks, observe, apply, the deferred
+// post point after the ticks), without the learner: no epsilon draw, no Q-table, no pending updates;
+// the post point only counts the step and checks max_steps (switch_env.py:652-657).
+template <int NW>
+SFL_FN void env_run_ext(const SflMap& m, const SflState& s, const SflCtl& c, uint32_t e) {
+  using V = Env<NW>;
+  const SflExt& x = *c.ext;
+  V v(m, s, e);
+  v.flags = s.eflags[e];
+  v.now = s.elapsed[e];
+  v.epoch = s.epoch[e];
+  v.err = s.err[e];
+  int32_t phase = s.phase[e];
+  uint64_t ticks = 0;
+  Decision d;
+  d.sw = d.h = d.slot = d.action = d.j = d.reward = d.next_sw = 0;
+  d.state = 0;
+  v.masks_load();
+  x.agent[e] = -1;
+  x.next_sw[e] = -1;
+  x.step_now[e] = -1;
+  const int32_t act = x.actions[e];
+  bool applied = false;
+  while (true) {
+    if (phase == PH_RESET) {
+      env_reset(v);
+      phase = PH_TICK;
+    } else if (phase == PH_TICK) {
+      env_tick(v);
+      ticks++;
+      if (v.flags & F_TERM) phase = (v.flags & F_INFLIGHT) ? PH_POST : PH_END;
+      else if (!queue_empty(v)) phase = (v.flags & F_INFLIGHT) ? PH_POST : PH_DECIDE;
+    } else if (phase == PH_DECIDE) {
+      if (!(v.flags & F_EXT_OBS) || applied || act < 0) {
+        // emit the observation of the queue's first train (agent_iter + last(); the queue is left
+        // as it is: the next call observes it again and applies the action)
+        uint32_t keep[NW];
+#pragma unroll
+        for (int w = 0; w < NW; ++w) keep[w] = v.msk[0][w];
+        Obs o;
+        decide_observe(v, o, true);
+#pragma unroll
+        for (int w = 0; w < NW; ++w) v.msk[0][w] = keep[w];
+        x.agent[e] = o.sw;
+        x.train[e] = o.h;
+        x.slot[e] = o.slot;
+        x.state[e] = o.state;
+        x.mask[e] = o.amask;
+        x.reward[e] = o.reward;
+        x.now[e] = v.now;
+        v.flags |= F_EXT_OBS;
+        break;
+      }
+      Obs o;
+      decide_observe(v, o, true);
+      decide_apply(v, o, act, d);
+      v.flags &= ~F_EXT_OBS;
+      v.flags |= F_INFLIGHT;
+      applied = true;
+      x.next_sw[e] = d.next_sw;
+      phase = queue_empty(v) ? PH_TICK : PH_POST;  // no active switch left: move the trains first
+    } else if (phase == PH_POST) {
+      // the step() of the applied action returns here (after the ticks when the queue emptied)
+      if (c.trace && (int32_t)e == c.trace_env) trace_decision(v, c, d);
+      v.flags &= ~F_INFLIGHT;
+      x.step_now[e] = v.now;
+      s.ep_dec[e] += 1;
+      s.dec_total[e] += 1;
+      s.step_ctr[e] += 1;
+      if (s.step_ctr[e] > m.max_steps) v.flags |= F_TRUNC;
+      phase = (v.flags & (F_TERM | F_TRUNC)) ? PH_END : PH_DECIDE;
+    } else {  // PH_END: report the episode (the learner records arrivals, delays, malfunctions)
+      for (int h = 0; h < m.T; ++h) x.delays[(size_t)h * s.E + e] = s.tr_delay[v.ix(h)];
+      x.n_mf[e] = s.n_mf[e];
+      x.truncated[e] = (v.flags & F_TRUNC) ? 1 : 0;
+      x.agent[e] = -1;
+      v.flags &= ~F_EXT_OBS;
+      phase = PH_RESET;
+      break;
+    }
+  }
+#pragma unroll
+  for (int w = 0; w < MAXW; ++w) x.arrived[(size_t)w * s.E + e] = w < NW ? v.msk[1][w < NW ? w : 0] : 0u;
+  v.masks_store();
+  s.phase[e] = phase;
+  s.elapsed[e] = v.now;
+  s.eflags[e] = v.flags;
+  s.epoch[e] = v.epoch;
+  s.err[e] = v.err;
+  if (c.launch_dec) c.launch_dec[e] = applied ? 1u : 0u;
+  if (c.launch_ticks) c.launch_ticks[e] = ticks;
+  if (c.launch_bytes) c.launch_bytes[e] = 0;
 }
 
 }  // namespace sfl

@@ -56,6 +56,12 @@ struct Handle {
   std::vector<uint32_t> h_row_base;
   // graph-partitioned mode (sfl_part.h); part.world == 0: not configured
   SflPart part{};
+  // external-action mode (sfl_env_begin / sfl_env_step): device buffers, the descriptor in device memory
+  SflExt ext{};
+  SflExt* d_ext = nullptr;
+  bool env_mode = false;
+  // per-phase cycles of the sampled wavefronts, accumulated over launches (sfl_get_phase_cycles)
+  uint64_t phase_cyc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 
   template <class T>
   T* dalloc(size_t n) {
@@ -539,6 +545,7 @@ int check_errors(Handle<B>* h) {
 template <class B>
 int run(Handle<B>* h, const SflCtl& c_in, sfl_run_args* args) {
   if (h->part.world) return fail("sfl_run: the handle is graph-partitioned; drive it with sfl_part_*");
+  if (h->env_mode) return fail("sfl_run: the handle is in external-action mode (sfl_env_begin); drive it with sfl_env_step");
   SflCtl c = c_in;
   const size_t E = h->E, T = h->map.T;
   const int32_t cap = args ? args->stats_cap : 0;
@@ -605,6 +612,101 @@ int run(Handle<B>* h, const SflCtl& c_in, sfl_run_args* args) {
   if (!rc) rc = h->be.sync();
   for (void* p : scratch) h->be.free(p);
   if (rc) return fail(std::string("sfl_run: ") + h->be.error());
+  return check_errors(h);
+}
+
+// ---------------------------------------------------------------------------
+// external-action mode (include/sfl.h sfl_env_begin / sfl_env_step; SflExt in sfl_core.h)
+// ---------------------------------------------------------------------------
+template <class B>
+int env_begin(Handle<B>* h) {
+  if (h->part.world) return fail("sfl_env_begin: the handle is graph-partitioned");
+  const size_t E = h->E, T = h->map.T, S = h->map.S, NP = h->map.NP;
+  if (!h->d_ext) {
+    SflExt& x = h->ext;
+    x.actions = h->template dalloc<int32_t>(E);
+    x.agent = h->template dalloc<int32_t>(E);
+    x.train = h->template dalloc<int32_t>(E);
+    x.slot = h->template dalloc<int32_t>(E);
+    x.state = h->template dalloc<uint32_t>(E);
+    x.mask = h->template dalloc<uint32_t>(E);
+    x.reward = h->template dalloc<int32_t>(E);
+    x.now = h->template dalloc<int32_t>(E);
+    x.next_sw = h->template dalloc<int32_t>(E);
+    x.step_now = h->template dalloc<int32_t>(E);
+    x.arrived = h->template dalloc<uint32_t>(MAXW * E);
+    x.n_mf = h->template dalloc<int32_t>(E);
+    x.delays = h->template dalloc<int32_t>(T * E);
+    x.truncated = h->template dalloc<int32_t>(E);
+    h->d_ext = h->template dalloc<SflExt>(1);
+    if (!x.actions || !x.agent || !x.train || !x.slot || !x.state || !x.mask || !x.reward || !x.now || !x.next_sw ||
+        !x.step_now || !x.arrived || !x.n_mf || !x.delays || !x.truncated || !h->d_ext)
+      return fail("sfl_env_begin: allocation failed");
+    h->be.h2d(h->d_ext, &h->ext, sizeof(SflExt));
+  }
+  // a fresh env (a new ASyncSwitchEnv): the lane-per-env body and its state layout, every env at reset
+  h->variant = 0;
+  h->env_mode = true;
+  SflState& st = h->st;
+  std::vector<int32_t> ph(E, PH_RESET);
+  h->be.h2d(st.phase, ph.data(), E * 4);
+  h->be.memset(st.eflags, 0, E * 4);
+  h->be.memset(st.elapsed, 0, E * 4);
+  h->be.memset(st.epoch, 0, E * 4);
+  h->be.memset(st.err, 0, E * 4);
+  h->be.memset(st.masks, 0, 4 * MAXW * E * 4);
+  h->be.memset(st.tr_pos, 0xFF, T * E * 4);
+  h->be.memset(st.tr_bits, 0, T * E * 4);
+  h->be.memset(st.tr_plan, 0, T * E * 4);
+  h->be.memset(st.tr_next, 0, T * E * 2);
+  h->be.memset(st.tr_prev, 0xFF, T * E * 2);
+  h->be.memset(st.tr_src, 0xFF, T * E * 2);
+  h->be.memset(st.tr_dec, 0, T * E * 2);
+  h->be.memset(st.own_n, 0, T * E);
+  h->be.memset(st.occ, 0xFF, (size_t)h->map.HW * E);
+  h->be.memset(st.claim, 0xFF, (size_t)h->map.HW * E);
+  h->be.memset(st.sem, 0, NP * E * 8);
+  h->be.memset(st.slot, 0, S * T * E * 8);
+  h->be.memset(st.step_ctr, 0, E * 8);
+  std::vector<int32_t> none(E, -1);
+  h->be.h2d((void*)h->ext.actions, none.data(), E * 4);
+  return h->be.sync() ? fail(h->be.error()) : 0;
+}
+
+template <class B>
+int env_step(Handle<B>* h, sfl_env_io* io) {
+  if (!h->env_mode) return fail("sfl_env_step: call sfl_env_begin first");
+  if (!io || !io->agent) return fail("sfl_env_step: null argument");
+  const size_t E = h->E, T = h->map.T;
+  const SflExt& x = h->ext;
+  if (io->actions) h->be.h2d((void*)x.actions, io->actions, E * 4);
+  else h->be.memset((void*)x.actions, 0xFF, E * 4);
+  SflCtl c{};
+  c.mode = 2;
+  c.ext = h->d_ext;
+  c.launch_dec = h->d_launch_dec;
+  c.launch_ticks = h->d_launch_ticks;
+  c.launch_bytes = h->d_launch_bytes;
+  float ms = 0.f;
+  if (h->be.run_ext(h->map, h->st, c, &ms)) return fail(std::string("sfl_env_step: ") + h->be.error());
+  h->last_kernel_ms = ms;
+  auto get = [&](void* dst, const void* src, size_t n) {
+    if (dst) h->be.d2h_async(dst, src, n);
+  };
+  get(io->agent, x.agent, E * 4);
+  get(io->train, x.train, E * 4);
+  get(io->slot, x.slot, E * 4);
+  get(io->state, x.state, E * 4);
+  get(io->mask, x.mask, E * 4);
+  get(io->reward, x.reward, E * 4);
+  get(io->now, x.now, E * 4);
+  get(io->next_switch, x.next_sw, E * 4);
+  get(io->step_now, x.step_now, E * 4);
+  get(io->arrived, x.arrived, MAXW * E * 4);
+  get(io->malfunctions, x.n_mf, E * 4);
+  get(io->delays, x.delays, T * E * 4);
+  get(io->truncated, x.truncated, E * 4);
+  if (h->be.sync()) return fail(std::string("sfl_env_step: ") + h->be.error());
   return check_errors(h);
 }
 

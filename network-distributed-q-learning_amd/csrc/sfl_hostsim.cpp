@@ -57,6 +57,16 @@ struct HostBackend {
     *ms = 0.f;
     return 0;
   }
+  int run_ext(const sfl::SflMap& m, const sfl::SflState& s, const sfl::SflCtl& c, float* ms) {
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int64_t e = 0; e < (int64_t)s.E; ++e) {
+      if (m.T <= 32) sfl::env_run_ext<1>(m, s, c, (uint32_t)e);
+      else if (m.T <= 64) sfl::env_run_ext<2>(m, s, c, (uint32_t)e);
+      else sfl::env_run_ext<4>(m, s, c, (uint32_t)e);
+    }
+    *ms = 0.f;
+    return 0;
+  }
   int sync() { return 0; }
   const uint32_t* seedseq_table() { return nullptr; }  // the host build draws every sub-generator
   void reduce_launch(const uint64_t* dec, const uint64_t* ticks, const uint64_t* bytes, const uint32_t* err, uint32_t E,

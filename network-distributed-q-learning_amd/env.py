@@ -6,10 +6,17 @@ runs on the GPU (csrc/sfl_core.h), so this class carries what the learner and th
 scripts read from the env — the compiled switch network, agent names, action
 spaces, ``max_steps``, the reset seed(s) and the timing accumulators
 (test_model.py:76-82) — and owns the device batch.
+
+It also speaks the AEC protocol itself for an external learner — ``reset(seed)``,
+``agent_iter()``, ``last()``, ``step(action)``, ``observe(agent)`` (switch_env.py:93,
+616-675) — on env 0 of an ``aec.AECBatch`` (the device's external-action mode: each
+``step`` is one ``sfl_env_step`` launch).
 """
 from __future__ import annotations
 
 from typing import List, Optional, Sequence, Union
+
+import numpy as np
 
 from . import compiler, mapgen, mfstream
 from . import observer as observer_mod
@@ -73,8 +80,107 @@ class ASyncSwitchEnv:
     def action_space(self, agent: str) -> Discrete:
         return self._spaces[agent]
 
+    # ---- the AEC protocol, env 0 of an external-action batch (switch_env.py:93, 616-675) ----------------
+    def reset(self, seed: Optional[int] = None, options=None, lib=None):
+        """Start an episode (switch_env.py:93-158) and run to its first decision.  A new seed (the
+        malfunction stream's, like rail_env.reset(random_seed=seed)) or a reset in the middle of an
+        episode starts a fresh device env; otherwise the env continues into its next episode (the trains'
+        previous / source ports carry over, as in the reference)."""
+        from .aec import AECBatch
+        import time
+        t0 = time.time()
+        seed = int(seed if seed is not None else (self.seed if self.seed is not None else 0))
+        aec = getattr(self, "_aec", None)
+        if aec is None or seed != self._aec_seed or lib is not None:
+            if aec is not None:
+                aec.close()
+            self._aec = AECBatch(self.compiled, [seed], lib=lib, device=self.device, max_steps=self.max_steps,
+                                 malfunction_stream=self.malfunction_stream, delay_threshold=self.delay_threshold)
+            self._aec_seed = seed
+            out = self._aec.step(None)
+        else:
+            out = self._aec.out
+            if out["agent"][0] >= 0:  # mid-episode: a fresh env
+                self._aec.lib.check(self._aec.lib.dll.sfl_env_begin(self._aec.batch.h), "sfl_env_begin")
+            out = self._aec.step(None)
+        self.terminated = self.truncated = False
+        self._pending()
+        self.reset_time += time.time() - t0
+        self.reset_total_time += time.time() - t0
+        return None
+
+    def _pending(self):
+        out = self._aec.out
+        s = int(out["agent"][0])
+        if s < 0:
+            self.agent_selection = None
+            self.active_train = None
+            return
+        self.agent_selection = self._aec.agent_name(s)
+        self.active_train = int(out["train"][0])
+
+    def agent_iter(self, max_iter: int = 2 ** 63):
+        """Yield the deciding switch agent until the episode terminates or is truncated (switch_env.py:616-630)."""
+        n = 0
+        while not (self.terminated or self.truncated) and n < max_iter and self.agent_selection is not None:
+            n += 1
+            yield self.agent_selection
+
+    def now(self) -> int:
+        """rail_env._elapsed_steps at the pending observation."""
+        return int(self._aec.out["now"][0])
+
+    def observe(self, agent: str) -> np.ndarray:
+        """observer.py:246-308 for the pending decision's agent."""
+        if agent != self.agent_selection:
+            raise ValueError(f"observe({agent}): only the deciding agent {self.agent_selection} has an observation")
+        return self._aec.observation(0)
+
+    def last(self, observe: bool = True):
+        """AECEnv.last(): (observation, rewards by train, termination, truncation, info) of the deciding agent;
+        the rewards map holds the active train's reward (switch_env.py:289: the reward its previous decision
+        delivered at this switch)."""
+        import time
+        t0 = time.time()
+        out = self._aec.out
+        obs = self._aec.observation(0) if observe else None
+        rew = {self.active_train: float(out["reward"][0])}
+        info = {"action_mask": self._aec.action_mask(0), "active_train": self.active_train}
+        self.last_time += time.time() - t0
+        return obs, rew, bool(self.terminated), bool(self.truncated), info
+
+    def step(self, action) -> dict:
+        """switch_env.py:632-666: apply the action, move the trains if no switch is active, and return
+        {"next_switch": (r, c), "arrived_trains": [handles]}."""
+        import time
+        if self.terminated or self.truncated or action is None or self.agent_selection is None:
+            return {}
+        if not self.action_space(self.agent_selection).contains(action):  # switch_env.py:213-215
+            raise AssertionError(f"action {action} outside {self.action_space(self.agent_selection)}")
+        t0 = time.time()
+        out = self._aec.step([int(action)])
+        nxt = int(out["next_switch"][0])
+        self.step_elapsed = int(out["step_now"][0])
+        arrived = self._aec.arrived_trains(0)
+        if out["agent"][0] < 0:  # the episode ended in this step
+            self.truncated = bool(out["truncated"][0])
+            self.terminated = not self.truncated
+            self.num_malfunctions = int(out["malfunctions"][0])
+            self.train_to_last_node_delays = [int(x) for x in out["delays"][:, 0]]
+        self._pending()
+        self.step_time += time.time() - t0
+        self.flatland_step_time += self._aec.batch.counters()["last_kernel_ms"] * 1e-3
+        return {"next_switch": tuple(self.compiled.switch_ids[nxt]), "arrived_trains": arrived}
+
+    def semaphores(self) -> dict:
+        """The port reservation table of env 0 in the reference's format (rail_network.semaphores)."""
+        return self._aec.semaphores(0)
+
     def get_num_agents(self) -> int:
         return self.compiled.T
 
     def close(self):
-        pass
+        aec = getattr(self, "_aec", None)
+        if aec is not None:
+            aec.close()
+            self._aec = None

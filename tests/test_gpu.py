@@ -460,3 +460,77 @@ def test_fallback_kernel_is_reported(lib, monkeypatch):
     monkeypatch.setenv("SFL_REQUIRE_WAVE", "1")
     with pytest.raises(_lib.SflError, match="256 switches"):
         runtime.Batch(cm, HP, [1, 2], lib=lib)
+
+
+# ---- round 3: the entry scripts on the GPU, the external-action (AEC) mode ---------------------------
+def _script(*args, timeout=600):
+    import os
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, *args], cwd=repo, capture_output=True, text=True, timeout=timeout)
+    assert r.returncode == 0, (args, r.stdout[-2000:], r.stderr[-4000:])
+    return r.stdout
+
+
+@pytest.mark.parametrize("name", ["c1_s7", "city6_s5"])
+def test_main_and_eval_scripts_gpu(lib, tmp_path, name):
+    """``python main.py -c config.ini`` then ``python eval.py EXP`` through libsfl.so (main.py:13-78,
+    eval.py:34-99): the .npz / .pkl outputs equal the golden vectors recorded from the reference."""
+    from tests import test_entrypoints as te
+    g, exp = te.prepare_golden_experiment(tmp_path, name)
+    out = _script("main.py", "-c", str(exp / "config.ini"))
+    assert "DONE!" in out
+    te.check_main_outputs(g, exp)
+    _script("eval.py", str(exp))
+    te.check_eval_outputs(g, exp)
+
+
+def test_main_script_flatland_stream_gpu(lib, tmp_path):
+    """``[ENV] malfunction_stream = flatland`` through main.py on libsfl.so equals the oracle."""
+    from tests import test_entrypoints as te
+    sc, hp, exp = te.prepare_flatland_stream_experiment(tmp_path)
+    _script("main.py", "-c", str(exp / "config.ini"))
+    te.check_flatland_stream_outputs(sc, hp, exp)
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_aec_replay_golden_gpu(lib, name):
+    """The external-action mode on the GPU: the reference's recorded actions replayed through
+    ASyncSwitchEnv.reset / agent_iter / last / step reproduce every golden decision and step event
+    (observation, reward, mask, successor, arrivals, time, semaphore-table digest)."""
+    from tests import aec_replay
+    g = _golden.load(name)
+    n = aec_replay.replay(g, g["learn"]["events"], lib)
+    assert n == sum(1 for e in g["learn"]["events"] if e[0] == "D")
+    aec_replay.replay(g, g["test"]["events"], lib)
+
+
+@pytest.mark.parametrize("cfg", ["c2", "c3"])
+def test_aec_batch_gpu_equals_host_build(lib, cfg):
+    """512 c2 and c3 envs stepped by a fixed policy through sfl_env_step: every output of every call equals
+    the host build's (bit-exact), c2 across episode ends."""
+    from tests import hostsim
+    aec = importlib.import_module("network-distributed-q-learning_amd.aec")
+    cm = comp.compile_scenario(mapgen.make_config(cfg))
+    seeds = [450565 + i for i in range(512)]
+    bg, bh = aec.AECBatch(cm, seeds, lib=lib), aec.AECBatch(cm, seeds, lib=hostsim.lib())
+    og, oh = bg.step(None), bh.step(None)
+    ends = 0
+    for k in range(400):
+        for key in og:
+            assert np.array_equal(og[key], oh[key]), (k, key)
+        acts = []
+        for e in range(len(seeds)):
+            s = int(og["agent"][e])
+            if s < 0:
+                acts.append(-1)
+                ends += 1
+                continue
+            m, n = int(og["mask"][e]), int(cm.n_actions[s])
+            allowed = [a for a in range(n) if (m >> a) & 1]
+            acts.append(allowed[(k + e) % len(allowed)])
+        og, oh = bg.step(acts), bh.step(acts)
+    assert ends > 0 or cfg != "c2"
+    bg.close()
+    bh.close()
