@@ -29,7 +29,7 @@ from __future__ import annotations
 import json
 import math
 from dataclasses import dataclass, field, asdict
-from typing import Dict, FrozenSet, List, Optional, Set, Tuple
+from typing import Dict, FrozenSet, List, Optional, Sequence, Set, Tuple
 
 import numpy as np
 
@@ -440,15 +440,45 @@ def _straight(r0: int, c0: int, r1: int, c1: int, pairs: Dict[Tuple[int, int], S
             pairs.setdefault((r, c0), set()).add(frozenset((N, S)))
 
 
+def _passing_loop(pairs, r0: int, c0: int, r1: int, c1: int, off: int):
+    """A second rail beside the plain segment (r0, c0) - (r1, c1) of one row or column, ``off`` cells in from
+    each end: T switches on the main line (trunks facing the segment's ends) and a parallel track two cells
+    below (rows) or right (columns) -- two rails between the segment's junctions, so trains meeting on it can
+    pass (Flatland's max_rails_between_cities = 2)."""
+    if r0 == r1:
+        xa, xb, rr = min(c0, c1) + off, max(c0, c1) - off, r0 + 2
+        pairs[(r0, xa)].add(frozenset((W, S)))
+        pairs[(r0, xb)].add(frozenset((E, S)))
+        _straight(r0, xa, rr, xa, pairs)
+        _straight(r0, xb, rr, xb, pairs)
+        pairs.setdefault((rr, xa), set()).add(frozenset((N, E)))
+        pairs.setdefault((rr, xb), set()).add(frozenset((N, W)))
+        _straight(rr, xa, rr, xb, pairs)
+        return [(r0, xa), (r0, xb)]
+    else:
+        ya, yb, cc = min(r0, r1) + off, max(r0, r1) - off, c0 + 2
+        pairs[(ya, c0)].add(frozenset((N, E)))
+        pairs[(yb, c0)].add(frozenset((S, E)))
+        _straight(ya, c0, ya, cc, pairs)
+        _straight(yb, c0, yb, cc, pairs)
+        pairs.setdefault((ya, cc), set()).add(frozenset((W, S)))
+        pairs.setdefault((yb, cc), set()).add(frozenset((W, N)))
+        _straight(ya, cc, yb, cc, pairs)
+        return [(ya, c0), (yb, c0)]
+
+
 def city_network(n_lines: int, spacing: int, margin: int, cities: List[Tuple[int, int, int]],
-                 rng: np.random.Generator, slip_weights=(0.2, 0.3, 0.5), size: Optional[int] = None):
+                 rng: np.random.Generator, slip_weights=(0.2, 0.3, 0.5), size: Optional[int] = None,
+                 rails: int = 1, loop_off: int = 4):
     """A square backbone of ``n_lines`` x ``n_lines`` rail lines (the inter-city connections) with
     cities on horizontal backbone segments, the way Flatland's sparse_rail_generator lays out a
     city: ``P`` parallel tracks (the backbone line plus P-1 sidings two rows apart) between two
     throats, each siding joining the main line through a T switch whose trunk faces out of the
     city.  ``cities``: (row line i, column line j, tracks P) -- the city sits between column lines
     j and j+1 on row line i.  ``size``: pad the grid to at least size x size (empty cells).  Returns
-    (grid, junction cells, per-city track cells, throat cells)."""
+    (grid, junction cells, per-city track cells, throat cells).  ``rails`` = 2: every backbone segment that
+    holds no city gets a passing loop (``_passing_loop``), the stand-in for Flatland's parallel inter-city
+    rails (max_rails_between_cities); a city's own parallel tracks already give its segment several rails."""
     side_len = max(size or 0, 2 * margin + (n_lines - 1) * spacing + 1)
     pos = [margin + k * spacing for k in range(n_lines)]
     pairs: Dict[Tuple[int, int], Set[FrozenSet[int]]] = {}
@@ -467,7 +497,7 @@ def city_network(n_lines: int, spacing: int, margin: int, cities: List[Tuple[int
     for (i, j, P) in cities:
         r0, cw, ce = pos[i], pos[j], pos[j + 1]
         a, b = cw + 2 * P, ce - 2 * P  # the city's platform span on every track
-        if b - a < 6 or (i + 1 < n_lines and pos[i + 1] - r0 < 2 * P + 2) or (i + 1 >= n_lines and 2 * P > margin + 1):
+        if b - a < (6 if P <= 3 else 4) or (i + 1 < n_lines and pos[i + 1] - r0 < 2 * P + 2) or (i + 1 >= n_lines and 2 * P > margin + 1):
             raise ValueError("city does not fit its backbone segment")
         tracks = [[(r0, c) for c in range(a + 1, b)]]
         for k in range(1, P):
@@ -484,6 +514,14 @@ def city_network(n_lines: int, spacing: int, margin: int, cities: List[Tuple[int
             _straight(rk, xw, rk, xe, pairs)
             tracks.append([(rk, c) for c in range(a + 1, b)])
         city_tracks.append(tracks)
+    if rails >= 2:
+        with_city = {(i, j) for (i, j, _) in cities}
+        for i in range(n_lines):
+            for j in range(n_lines - 1):
+                if (i, j) not in with_city and pos[j + 1] - pos[j] >= 2 * loop_off + 3:
+                    junctions.update(_passing_loop(pairs, pos[i], pos[j], pos[i], pos[j + 1], loop_off))
+                if pos[j + 1] - pos[j] >= 2 * loop_off + 3:
+                    junctions.update(_passing_loop(pairs, pos[j], pos[i], pos[j + 1], pos[i], loop_off))
     grid = np.zeros((side_len, side_len), dtype=np.int64)
     for (r, c), prs in pairs.items():
         grid[r, c] = pairs_to_bits(prs)
@@ -493,7 +531,7 @@ def city_network(n_lines: int, spacing: int, margin: int, cities: List[Tuple[int
 def generate_cities(n_cities: int, n_trains: int, seed: int, *, n_lines: Optional[int] = None, spacing: int = 20,
                     margin: int = 7, tracks: Tuple[int, int] = (2, 3), malfunction: Tuple[float, int, int] = (0.0, 0, 0),
                     name: str = "", slip_weights=(0.2, 0.3, 0.5), max_tries: int = 200,
-                    size: Optional[int] = None) -> Scenario:
+                    size: Optional[int] = None, rails: int = 1, track_choices: Optional[Sequence[int]] = None) -> Scenario:
     """Flatland-like scenario: ``n_cities`` cities of 2-3 parallel tracks with one station each on a
     square backbone of inter-city lines; every train starts on a city track and targets the station
     of another city; timetable as flatland_patch/timetable_generators.py (``timetable``)."""
@@ -507,9 +545,13 @@ def generate_cities(n_cities: int, n_trains: int, seed: int, *, n_lines: Optiona
     rng = np.random.default_rng(seed)
     for _ in range(max_tries):
         pick = sorted(int(x) for x in rng.choice(len(slots), size=n_cities, replace=False))
-        cities = [(slots[q][0], slots[q][1], int(rng.integers(tracks[0], tracks[1] + 1))) for q in pick]
+        if track_choices:  # Flatland: 2 * randint(1, max_rail_pairs_in_city + 1) tracks per city
+            cities = [(slots[q][0], slots[q][1], int(track_choices[int(rng.integers(0, len(track_choices)))]))
+                      for q in pick]
+        else:
+            cities = [(slots[q][0], slots[q][1], int(rng.integers(tracks[0], tracks[1] + 1))) for q in pick]
         grid, junctions, city_tracks, throats = city_network(n_lines, spacing, margin, cities, rng, slip_weights,
-                                                             size=size)
+                                                             size=size, rails=rails)
         if not strongly_connected(grid):
             continue
         near_junction = lambda rc: any((rc[0] + dr, rc[1] + dc) in junctions for dr, dc in DELTA)  # noqa: E731
@@ -593,15 +635,23 @@ def from_flatland_params(width: int, height: int, max_num_cities: int, number_of
     ``max_num_cities`` is a cap, as in Flatland, which places as many cities as fit -- here the
     largest backbone that fits the grid decides.  With one city, or a grid too small for a backbone
     (< 51 cells), a line grid of that size with one station per city.
-    ``max_rails_between_cities`` / ``max_rail_pairs_in_city`` have no counterpart in the stand-in
-    layout (a warning says so when they are given)."""
+    ``max_rails_between_cities`` >= 2 gives every backbone segment without a city a passing loop (two rails
+    between its junctions; a city's segment has its own parallel tracks); ``max_rail_pairs_in_city`` = k gives
+    each city 2 * randint(1, k + 1) tracks, as Flatland draws them.  Left out (None), the round-2 layout:
+    single-track backbone, 2-3 tracks per city."""
     import warnings
     size = max(int(width), int(height))
     n_cities, n_agents = int(max_num_cities), int(number_of_agents)
-    if max_rails_between_cities is not None or max_rail_pairs_in_city is not None:
-        warnings.warn("max_rails_between_cities / max_rail_pairs_in_city are ignored: the map is mapgen's stand-in "
-                      "layout, not Flatland's sparse_rail_generator (absent)", stacklevel=2)
-    n_fit = (size - 2 * CITY_MARGIN - 1) // CITY_SPACING + 1  # backbone lines that fit the grid
+    rails = int(max_rails_between_cities) if max_rails_between_cities is not None else 1
+    choices = None
+    spacing_need = CITY_SPACING
+    if max_rail_pairs_in_city is not None:
+        choices = [2 * k for k in range(1, max(1, int(max_rail_pairs_in_city)) + 1)]
+        spacing_need = max(CITY_SPACING if max(choices) <= 3 else 0, 4 * max(choices) + 4)
+    if rails > 2:
+        warnings.warn(f"max_rails_between_cities={rails}: the stand-in layout lays at most two rails per segment",
+                      stacklevel=2)
+    n_fit = (size - 2 * CITY_MARGIN - 1) // spacing_need + 1  # backbone lines that fit the grid
     if n_cities >= 2 and n_fit >= 3:  # (a two-line backbone is a loop a train cannot turn around on)
         n_lines = 3
         while n_lines * (n_lines - 1) < n_cities and n_lines < n_fit:
@@ -613,7 +663,7 @@ def from_flatland_params(width: int, height: int, max_num_cities: int, number_of
         c_spacing = (size - 2 * CITY_MARGIN - 1) // (n_lines - 1)
         return generate_cities(n_cities, n_agents, seed=int(seed), n_lines=n_lines, spacing=c_spacing,
                                margin=CITY_MARGIN, malfunction=malfunction, name=f"flatland_{width}x{height}",
-                               size=size)
+                               size=size, rails=rails, track_choices=choices)
     n_lines = max(3, (size - 2 * margin - 1) // spacing + 1)
     n_sw = n_lines * n_lines - 4
     return generate(n_switches=n_sw, n_trains=n_agents, n_stations=max(1, min(n_cities, n_agents)), seed=int(seed),

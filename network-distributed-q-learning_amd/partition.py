@@ -80,11 +80,13 @@ class PartitionedBatch:
     def __init__(self, cm: CompiledMap, hp: dict, seeds: Sequence[int], env_base: int, envs_total: int,
                  rank: int = 0, world: int = 1, dist=None, lib: Optional[_lib.Lib] = None, device: int = 0,
                  owner: Optional[np.ndarray] = None, upd_per_env: int = 16, ntab: Optional[int] = None,
-                 buffer_device: str = "cuda", local_rows=True, malfunction_stream: str = "counter"):
+                 buffer_device: str = "cuda", local_rows=True, malfunction_stream: str = "counter",
+                 delay_threshold: int = 20):
         import torch
         self.torch = torch
         kw = {} if ntab is None else dict(ntab=ntab)
         kw["malfunction_stream"] = malfunction_stream
+        kw["delay_threshold"] = int(delay_threshold)  # StandardObserver(delay_threshold=...), observer.py:221
         self.batch = Batch(cm, hp, seeds, lib=lib, device=device, **kw)
         self.lib = self.batch.lib
         self.cm, self.rank, self.world, self.dist = cm, int(rank), int(world), dist
@@ -97,7 +99,9 @@ class PartitionedBatch:
         if e_sum != self.envs_total:
             raise ValueError(f"envs_total={self.envs_total} but the ranks hold {e_sum} envs")
         self.cap_req = e_max
-        self.cap_upd = max(64, upd_per_env * self.E)
+        # a rank with more envs may send more update records to a smaller rank than 16 per receiver env:
+        # size every update segment from the job's largest shard, like the request segments
+        self.cap_upd = max(64, upd_per_env * e_max)
         self.lib.check(self.lib.dll.sfl_part_config(self.batch.h, self.rank, self.world, _ptr(self.owner, C.c_int32),
                                                     self.env_base, self.envs_total, self.cap_req, self.cap_upd),
                        "sfl_part_config")

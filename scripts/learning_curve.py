@@ -35,6 +35,8 @@ def main():
     ap.add_argument("--layout", default="cities", choices=["cities", "grid"],
                     help="cities: main.py's [ENV] keys (mapgen.from_flatland_params, city stand-in); grid: a line-grid "
                          "stand-in with the same trains (mapgen.generate, 60 switches, 8 stations)")
+    ap.add_argument("--rails", type=int, default=2, help="max_rails_between_cities (the sweep: 2)")
+    ap.add_argument("--pairs", type=int, default=2, help="max_rail_pairs_in_city (the sweep: 2)")
     args = ap.parse_args()
     mapgen = importlib.import_module(PKG + ".mapgen")
     comp = importlib.import_module(PKG + ".compiler")
@@ -44,7 +46,8 @@ def main():
         from tests import hostsim
         lib = hostsim.lib()
     hp = dict(gamma=1.0, epsilon=0.5, epsilon_decay_rate=0.9997, lr=0.1, lr_decay_rate=1.0, default_q=0.0)
-    res = {"config": "hyperparam_tuning.py:10-35 (80x80, max_num_cities 25, 15 trains, no malfunctions)",
+    res = {"config": "hyperparam_tuning.py:10-35 (80x80, max_num_cities 25, max_rails_between_cities "
+                     f"{args.rails}, max_rail_pairs_in_city {args.pairs}, 15 trains, no malfunctions)",
            "layout": args.layout,
            "episodes": args.episodes, "exploit_freq": args.exploit_freq, "hparams": hp, "seeds": {}}
     t_all = time.time()
@@ -52,7 +55,9 @@ def main():
         with warnings.catch_warnings():
             warnings.simplefilter("ignore")
             if args.layout == "cities":
-                sc = mapgen.from_flatland_params(80, 80, 25, 15, seed, malfunction=(0.0, 0, 0))
+                # the sweep's [ENV] keys (hyperparam_tuning.py:17-25), as main.py passes them
+                sc = mapgen.from_flatland_params(80, 80, 25, 15, seed, malfunction=(0.0, 0, 0),
+                                                 max_rails_between_cities=args.rails, max_rail_pairs_in_city=args.pairs)
             else:
                 sc = mapgen.generate(60, 15, 8, seed=seed)
         cm = comp.compile_scenario(sc)

@@ -138,3 +138,13 @@ def test_generator_rejects_bad_arguments():
     rc = lib.dll.sfl_mf_schedule_flatland(k.ctypes.data_as(P(C.c_uint32)), 2, None, 0, 2, 0.5, 9, 5, 4,
                                           out.ctypes.data_as(P(C.c_uint8)))
     assert rc != 0
+
+
+def test_schedule_refuses_oversized_tables(monkeypatch):
+    """The [E][steps][T] proposal table fails early, with a message, above the size cap."""
+    import pytest
+    from tests import hostsim
+    sc = mapgen.make_config("c2", malfunction=(0.05, 3, 9))
+    monkeypatch.setenv("SFL_MF_TABLE_MAX_BYTES", str(1000))
+    with pytest.raises(ValueError, match="GiB"):
+        mfstream.schedule(hostsim.lib(), sc, [1, 2, 3])
