@@ -42,10 +42,12 @@ __global__ void __launch_bounds__(256) k_run_ext(const sfl::SflMap* __restrict__
 
 // One env per wavefront (sfl_wave.h): 4 envs per block.  PPL / SPL = semaphore / counter
 // registers per lane (sfl::kVariants).
-template <int PPL, int SPL, int TW, bool TRACE>
+// TIMED: the learn() / test() instantiation, with the sampled phase timers (sfl_wave.h PhaseTimer); the
+// benchmark's sfl_step runs the untimed one
+template <int PPL, int SPL, int TW, bool TRACE, bool TIMED = false>
 __global__ void __launch_bounds__(SFL_WAVE_BLOCK) __attribute__((amdgpu_waves_per_eu(SFL_WAVE_OCC))) k_wave(const sfl::SflMap* __restrict__ m, const sfl::SflState* __restrict__ s,
                                               const sfl::SflCtl* __restrict__ c) {
-  sfl::wave::run<PPL, SPL, TW, TRACE>(*m, *s, *c);
+  sfl::wave::run<PPL, SPL, TW, TRACE, false, TIMED>(*m, *s, *c);
 }
 // several envs per wavefront (sfl_wave.h run_groups): G lanes per env, SFL_WAVE_BLOCK / G envs per block
 // waves per SIMD the grouped kernel is register-budgeted for: shapes with one train slot per lane
@@ -58,21 +60,21 @@ __global__ void __launch_bounds__(SFL_WAVE_BLOCK) __attribute__((amdgpu_waves_pe
 #ifndef SFL_GROUP_OCC
 #define SFL_GROUP_OCC (SFL_PF_RING > 0 ? 4 : 3)  // two slots per lane: 4 with the prefetch ring (LDS 4 blocks/CU)
 #endif
-template <int PPL, int SPL, int TW, bool TRACE, int G>
+template <int PPL, int SPL, int TW, bool TRACE, int G, bool TIMED = false>
 __global__ void __launch_bounds__(SFL_WAVE_BLOCK) __attribute__((amdgpu_waves_per_eu(TW <= G ? SFL_GROUP_OCC1 : SFL_GROUP_OCC)))
 k_wave_g(const sfl::SflMap* __restrict__ m, const sfl::SflState* __restrict__ s, const sfl::SflCtl* __restrict__ c) {
-  sfl::wave::run_groups<PPL, SPL, TW, TRACE, G>(*m, *s, *c);
+  sfl::wave::run_groups<PPL, SPL, TW, TRACE, G, TIMED>(*m, *s, *c);
 }
 // maps with 65-128 trains (two train slots per lane): one env per 64-thread block (its LDS is
 // ~22 KB), register budget for the LDS-bound occupancy of 2 waves per SIMD
 #ifndef SFL_WAVE2_OCC
 #define SFL_WAVE2_OCC (SFL_PF_RING64 > 0 ? 4 : 2)  // waves per SIMD k_wave2 is register-budgeted for
 #endif
-template <int PPL, int SPL, int TW, bool TRACE>
+template <int PPL, int SPL, int TW, bool TRACE, bool TIMED = false>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SFL_WAVE2_OCC))) k_wave2(const sfl::SflMap* __restrict__ m,
                                                                                    const sfl::SflState* __restrict__ s,
                                                                                    const sfl::SflCtl* __restrict__ c) {
-  sfl::wave::run<PPL, SPL, TW, TRACE>(*m, *s, *c);
+  sfl::wave::run<PPL, SPL, TW, TRACE, false, TIMED>(*m, *s, *c);
 }
 
 // graph-partitioned rounds, local env step on the one-env-per-wave body (sfl_wave.h, PART)
@@ -453,24 +455,33 @@ struct HipBackend {
     const auto* pc = (const sfl::SflCtl*)(base + oc);
     const unsigned wblocks = (unsigned)(((size_t)s.E * 64 + SFL_WAVE_BLOCK - 1) / SFL_WAVE_BLOCK);
 #define SFL_KW(v)                                                                                                   \
-  (c.trace ? k_wave<sfl::kVariants[v].PPL, sfl::kVariants[v].SPL, sfl::kVariants[v].TW, true><<<wblocks, SFL_WAVE_BLOCK, 0, stream>>>(pm, ps, pc) \
-           : k_wave<sfl::kVariants[v].PPL, sfl::kVariants[v].SPL, sfl::kVariants[v].TW, false><<<wblocks, SFL_WAVE_BLOCK, 0, stream>>>(pm, ps, pc))
+  {                                                                                                             \
+    constexpr sfl::WaveShape w = sfl::kVariants[v];                                                             \
+    if (c.trace) k_wave<w.PPL, w.SPL, w.TW, true><<<wblocks, SFL_WAVE_BLOCK, 0, stream>>>(pm, ps, pc);          \
+    else if (c.phase_cyc) k_wave<w.PPL, w.SPL, w.TW, false, true><<<wblocks, SFL_WAVE_BLOCK, 0, stream>>>(pm, ps, pc); \
+    else k_wave<w.PPL, w.SPL, w.TW, false><<<wblocks, SFL_WAVE_BLOCK, 0, stream>>>(pm, ps, pc);                 \
+  }
 #define SFL_KW2(v)                                                                                       \
-  (c.trace ? k_wave2<sfl::kVariants[v].PPL, sfl::kVariants[v].SPL, sfl::kVariants[v].TW, true><<<s.E, 64, 0, stream>>>(pm, ps, pc) \
-           : k_wave2<sfl::kVariants[v].PPL, sfl::kVariants[v].SPL, sfl::kVariants[v].TW, false><<<s.E, 64, 0, stream>>>(pm, ps, pc))
+  {                                                                                                             \
+    constexpr sfl::WaveShape w = sfl::kVariants[v];                                                             \
+    if (c.trace) k_wave2<w.PPL, w.SPL, w.TW, true><<<s.E, 64, 0, stream>>>(pm, ps, pc);                         \
+    else if (c.phase_cyc) k_wave2<w.PPL, w.SPL, w.TW, false, true><<<s.E, 64, 0, stream>>>(pm, ps, pc);         \
+    else k_wave2<w.PPL, w.SPL, w.TW, false><<<s.E, 64, 0, stream>>>(pm, ps, pc);                                \
+  }
 #define SFL_KG(v)                                                                                               \
   {                                                                                                             \
     constexpr sfl::WaveShape w = sfl::kVariants[v];                                                             \
     const unsigned gblocks = (unsigned)(((size_t)s.E * w.G + SFL_WAVE_BLOCK - 1) / SFL_WAVE_BLOCK);             \
     if (c.trace) k_wave_g<w.PPL, w.SPL, w.TW, true, w.G><<<gblocks, SFL_WAVE_BLOCK, 0, stream>>>(pm, ps, pc);    \
+    else if (c.phase_cyc) k_wave_g<w.PPL, w.SPL, w.TW, false, w.G, true><<<gblocks, SFL_WAVE_BLOCK, 0, stream>>>(pm, ps, pc); \
     else k_wave_g<w.PPL, w.SPL, w.TW, false, w.G><<<gblocks, SFL_WAVE_BLOCK, 0, stream>>>(pm, ps, pc);          \
   }
     static_assert(sfl::kVariants[5].TW > 64 && sfl::kNumVariants == 10, "variant 5 is the two-slot shape, 6-9 grouped");
-    if (variant == 1) SFL_KW(1);
-    else if (variant == 2) SFL_KW(2);
-    else if (variant == 3) SFL_KW(3);
-    else if (variant == 4) SFL_KW(4);
-    else if (variant == 5) SFL_KW2(5);
+    if (variant == 1) SFL_KW(1)
+    else if (variant == 2) SFL_KW(2)
+    else if (variant == 3) SFL_KW(3)
+    else if (variant == 4) SFL_KW(4)
+    else if (variant == 5) SFL_KW2(5)
     else if (variant == 6) SFL_KG(6)
     else if (variant == 7) SFL_KG(7)
     else if (variant == 8) SFL_KG(8)

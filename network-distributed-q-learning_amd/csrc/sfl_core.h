@@ -179,6 +179,7 @@ struct SflCtl {
   int32_t trace_env;
   int32_t trace_cap;
   const struct SflExt* ext;  // external-action mode (mode 2) buffers, device memory; null otherwise
+  uint64_t* phase_cyc;       // [8] per-phase cycles of sampled wavefronts (learn / test launches), or null
 };
 
 // External-action mode (sfl_env_step): the env alone, stepped one decision per call by a policy on the

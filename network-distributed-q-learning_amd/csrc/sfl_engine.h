@@ -60,8 +60,9 @@ struct Handle {
   SflExt ext{};
   SflExt* d_ext = nullptr;
   bool env_mode = false;
-  // per-phase cycles of the sampled wavefronts, accumulated over launches (sfl_get_phase_cycles)
-  uint64_t phase_cyc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  // per-phase cycles of the sampled wavefronts, accumulated over learn / test launches on the device
+  // (sfl_get_phase_cycles reads them)
+  uint64_t* d_phase = nullptr;
 
   template <class T>
   T* dalloc(size_t n) {
@@ -370,6 +371,7 @@ int create(const sfl_map_desc* md, const sfl_hparams* hp, uint32_t n_envs, const
   h->d_launch_ticks = h->template dalloc<uint64_t>(E);
   h->d_launch_bytes = h->template dalloc<uint64_t>(E);
   h->d_sums = h->template dalloc<uint64_t>(4);
+  h->d_phase = h->template dalloc<uint64_t>(8);
   for (void* p : h->allocs)
     if (!p) {
       delete h;
@@ -409,6 +411,7 @@ int create(const sfl_map_desc* md, const sfl_hparams* hp, uint32_t n_envs, const
   h->be.memset(s.sem, 0, NP * E * 8);
   h->be.memset(s.slot, 0, S * T * E * 8);
   h->be.memset(s.counts, 0, S * E * 4);
+  h->be.memset(h->d_phase, 0, 8 * 8);
   h->be.memset(s.touched, 0, (size_t)m.touched_words * E * 4);
   h->be.fill_f64(s.q, m.default_q, (size_t)m.q_per_env * E);
   h->seeds.assign(env_seeds, env_seeds + E);
@@ -577,6 +580,7 @@ int run(Handle<B>* h, const SflCtl& c_in, sfl_run_args* args) {
   c.launch_dec = h->d_launch_dec;
   c.launch_ticks = h->d_launch_ticks;
   c.launch_bytes = h->d_launch_bytes;
+  c.phase_cyc = args ? h->d_phase : nullptr;  // learn / test (not the benchmark's sfl_step): phase timers
   uint64_t* d_trace = nullptr;
   uint64_t* d_trace_n = nullptr;
   if (args && args->trace && args->trace_cap > 0) {

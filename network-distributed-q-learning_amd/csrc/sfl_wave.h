@@ -336,6 +336,11 @@ struct WEnv {
   uint32_t n_upd = 0;      // update records staged
   uint32_t stg = 0;        // next update stage of this launch (the posts' records in program order)
   uint32_t sem0[PART ? PPL : 1], cnt0[PART ? SPL : 1];  // the launch's loaded records / counters
+  // product phase timers (the TIMED kernels that learn() / test() run; sfl_get_phase_cycles): decide<true>
+  // stamps the end of its observe and epsilon-greedy sections on a sampled wavefront (tm_on); run_groups
+  // reads the stamps from a deciding lane after the (divergent) decide block
+  bool tm_on = false;
+  uint64_t tm_obs_t = 0, tm_eg_t = 0;
 #ifdef SFL_PROFILE
   uint64_t prof[9] = {};  // decide: observe, epsilon-greedy, apply; events: prefetch, row hit/miss, pend hit/miss, decisions
   uint64_t lap[16] = {};  // finer segments (see SFL_LAP call sites)
@@ -1408,6 +1413,7 @@ struct WEnv {
   // PART: true = observe pass (no reply yet): the request went to the row's owner and nothing of
   // the env changed (the next launch repeats the observation, which is deterministic, and
   // applies the reply)
+  template <bool TM = false>
   __device__ __forceinline__ bool decide(Dec& d, bool greedy) {
     // PART: a row of this rank's own switches is decided in one pass, like the fused kernel
     const bool loc = local_sw((int)(trl(sdec, mctz(q_mask)) >> 16));
@@ -1485,6 +1491,9 @@ struct WEnv {
         ((uint32_t)BAL(lid() < na - 1 && srca == (uint32_t)slot && ((free_bits >> dsta) & 1u)) & 0xFFu) |
         (1u << (na - 1));
     SFL_LAP(3);
+    if constexpr (TM) {  // observe done (observer.py:246-308)
+      if (tm_on) tm_obs_t = (uint64_t)__builtin_amdgcn_s_memtime();
+    }
     SFL_PACC(0, t_obs);
     SFL_PT(t_eg);
     // issue the Q row load and the pending update's Q cell load, then draw while they fly
@@ -1632,6 +1641,9 @@ struct WEnv {
     action = U(action);
     if (action < 0 || action >= na) lerr |= E_BAD_ACTION;
     SFL_LAP(7);
+    if constexpr (TM) {  // action selected (distr_q.py:312-319)
+      if (tm_on) tm_eg_t = (uint64_t)__builtin_amdgcn_s_memtime();
+    }
     SFL_PACC(1, t_eg);
     SFL_PT(t_ap);
     // _apply_action
@@ -1964,7 +1976,61 @@ struct WEnv {
 // PART: one round of the graph-partitioned mode (P = its tables and this round's message
 // buffers): each env applies the reply to its open request, runs to its next decision and stops
 // after emitting that decision's request; c.dec_budget counts decisions since sfl_part_begin
-template <int PPL, int SPL, int TW, bool TRACE, bool PART = false>
+// phase-timer buckets (SflCtl::phase_cyc, include/sfl.h sfl_get_phase_cycles)
+enum { TM_TICK = 0, TM_OBS = 1, TM_EG = 2, TM_APPLY = 3, TM_POST = 4, TM_RESET = 5, TM_OTHER = 6, TM_TOTAL = 7 };
+// the TIMED kernels sample one wavefront in TM_SAMPLE blocks
+constexpr uint32_t TM_SAMPLE = 8;
+struct PhaseTimer {
+  bool on;
+  uint64_t t, acc[8];
+  __device__ __forceinline__ void start(bool on_) {
+    on = on_;
+    t = on ? (uint64_t)__builtin_amdgcn_s_memtime() : 0ull;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[k] = 0ull;
+    acc[TM_TOTAL] = t;
+  }
+  __device__ __forceinline__ void lap(int k) {
+    if (on) {
+      const uint64_t n = (uint64_t)__builtin_amdgcn_s_memtime();
+      acc[k] += n - t;
+      t = n;
+    }
+  }
+  // the decide block split at decide's stamps, read from lane `lane` (a lane that decided; -1: none did)
+  template <class V>
+  __device__ __forceinline__ void decide_done(const V& v, int lane) {
+    if (on) {
+      const uint64_t n = (uint64_t)__builtin_amdgcn_s_memtime();
+      if (lane >= 0) {
+        const uint64_t o = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(v.tm_obs_t >> 32), lane) << 32) |
+                           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v.tm_obs_t, lane);
+        const uint64_t g = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(v.tm_eg_t >> 32), lane) << 32) |
+                           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v.tm_eg_t, lane);
+        acc[TM_OBS] += o - t;
+        acc[TM_EG] += g - o;
+        acc[TM_APPLY] += n - g;
+      } else {
+        acc[TM_OTHER] += n - t;
+      }
+      t = n;
+    }
+  }
+  __device__ __forceinline__ void flush(const SflCtl& c) {
+    if (!on) return;
+    const uint64_t end = (uint64_t)__builtin_amdgcn_s_memtime();
+    acc[TM_TOTAL] = end - acc[TM_TOTAL];
+    uint64_t known = 0;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) known += acc[k];
+    acc[TM_OTHER] = acc[TM_TOTAL] > known ? acc[TM_TOTAL] - known : 0ull;
+    if (__lane_id() == 0)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) atomicAdd((unsigned long long*)&c.phase_cyc[k], (unsigned long long)acc[k]);
+  }
+};
+
+template <int PPL, int SPL, int TW, bool TRACE, bool PART = false, bool TIMED = false>
 __device__ void run(const SflMap& m, const SflState& s, const SflCtl& c, const SflPart* P = nullptr) {
   using V = WEnv<PPL, SPL, TW, PART>;
   // semaphores, counters, prefetch records, rng, timetable (PART: one record, timetable from the map)
@@ -1975,6 +2041,8 @@ __device__ void run(const SflMap& m, const SflState& s, const SflCtl& c, const S
   constexpr int WPB = TW > 64 ? 1 : SFL_WAVE_BLOCK / 64;  // waves (envs) per block (sfl.hip launches)
   __shared__ uint32_t lds[WPB * LDS_WORDS];
   V v(m, s, e, lane, lds + (threadIdx.x >> 6) * LDS_WORDS, P);
+  PhaseTimer tm;
+  if constexpr (TIMED) tm.start(c.phase_cyc != nullptr && blockIdx.x % TM_SAMPLE == 0u);
   v.load();
   if constexpr (xp::kLoadTwice) v.load();  // experiment build: the marginal cost of the state load
   const int64_t dec_base = PART ? (int64_t)uni((uint64_t)ld(P->dec_done, e)) : 0;
@@ -2009,13 +2077,17 @@ __device__ void run(const SflMap& m, const SflState& s, const SflCtl& c, const S
         else v.flags &= ~F_GREEDY;
       }
       SFL_PT(t0);
+      if constexpr (TIMED) tm.lap(TM_OTHER);
       v.reset();
+      if constexpr (TIMED) tm.lap(TM_RESET);
       SFL_PACC(0, t0);
       phase = PH_TICK;
     } else if (phase == PH_TICK) {
       abytes += 36u * (uint32_t)(m.T - mpopc(v.arr_mask));
       SFL_PT(t0);
+      if constexpr (TIMED) tm.lap(TM_OTHER);
       v.tick();
+      if constexpr (TIMED) tm.lap(TM_TICK);
       SFL_PACC(1, t0);
       ticks++;
       if (v.flags & F_TERM) phase = (v.flags & F_INFLIGHT) ? PH_POST : PH_END;
@@ -2025,7 +2097,9 @@ __device__ void run(const SflMap& m, const SflState& s, const SflCtl& c, const S
       // post step + loop bookkeeping of decision d; true: the launch's decision budget is spent
       auto finish = [&]() -> bool {
         SFL_PT(t0);
+        if constexpr (TIMED) tm.lap(TM_OTHER);
         v.post(d, greedy);
+        if constexpr (TIMED) tm.lap(TM_POST);
         SFL_PACC(3, t0);
         if (TRACE && c.trace && (int32_t)e == c.trace_env) {
           const uint64_t cs = v.sem_checksum();
@@ -2062,7 +2136,12 @@ __device__ void run(const SflMap& m, const SflState& s, const SflCtl& c, const S
             break;
           }
           SFL_PT(t0);
-          const bool requested = v.decide(d, greedy);
+          if constexpr (TIMED) {
+            tm.lap(TM_OTHER);
+            v.tm_on = tm.on;
+          }
+          const bool requested = v.template decide<TIMED>(d, greedy);
+          if constexpr (TIMED) tm.decide_done(v, 0);
           SFL_PACC(2, t0);
           if (PART && requested) {
             stop = true;  // the round ends at the request (phase stays PH_DECIDE)
@@ -2115,6 +2194,7 @@ __device__ void run(const SflMap& m, const SflState& s, const SflCtl& c, const S
   }
   v.store(phase);
   if constexpr (xp::kStoreTwice) v.store(phase);  // experiment build: the marginal cost of the state store
+  if constexpr (TIMED) tm.flush(c);
 #ifdef SFL_PROFILE
   prof[4] = (uint64_t)__builtin_amdgcn_s_memtime() - t_begin;
   if (lane == 0) {
@@ -2142,7 +2222,7 @@ __device__ void run(const SflMap& m, const SflState& s, const SflCtl& c, const S
 // follow it -- as a flat loop in which each iteration advances every group by at most one tick,
 // one post step and one decision.  The groups of a wave diverge (one ticks while another decides);
 // a batch loop as in run() would hold every group until the longest batch of the wave is done.
-template <int PPL, int SPL, int TW, bool TRACE, int G>
+template <int PPL, int SPL, int TW, bool TRACE, int G, bool TIMED = false>
 __device__ void run_groups(const SflMap& m, const SflState& s, const SflCtl& c) {
   using V = WEnv<PPL, SPL, TW, false, G>;
   // per env: semaphores, counters, prefetch records, rng; per block: the timetable rows and the
@@ -2165,6 +2245,8 @@ __device__ void run_groups(const SflMap& m, const SflState& s, const SflCtl& c) 
   v.tsw = lds + O_SW;
   v.tpp = lds + O_PP;
   v.tpt = lds + O_PT;
+  PhaseTimer tm;
+  if constexpr (TIMED) tm.start(c.phase_cyc != nullptr && blockIdx.x % TM_SAMPLE == 0u && threadIdx.x < 64u);
   v.load();
   int32_t phase = ld(s.phase, e);
   int32_t ep_t = ld(s.ep_t, e), n_test = ld(s.n_test, e);
@@ -2217,6 +2299,7 @@ __device__ void run_groups(const SflMap& m, const SflState& s, const SflCtl& c) 
       v.reset();
       phase = PH_TICK;
     }
+    if constexpr (TIMED) tm.lap(TM_RESET);
 #ifndef SFL_GROUP_NOSYNC
     // the groups waiting for a tick start it once fewer than SFL_TICK_HOLD groups can still
     // decide: their ticks then run together, while the last deciding group (if any) runs its
@@ -2231,6 +2314,7 @@ __device__ void run_groups(const SflMap& m, const SflState& s, const SflCtl& c) 
 #ifdef SFL_PROFILE
     tp0 = __builtin_amdgcn_s_memtime();
 #endif
+    if constexpr (TIMED) tm.lap(TM_OTHER);
     if (phase == PH_TICK && !wave_decides) {
       abytes += 36u * (uint32_t)(m.T - mpopc(v.arr_mask));
       v.tick();
@@ -2238,6 +2322,7 @@ __device__ void run_groups(const SflMap& m, const SflState& s, const SflCtl& c) 
       if (v.flags & F_TERM) phase = (v.flags & F_INFLIGHT) ? PH_POST : PH_END;
       else if (many(v.q_mask)) phase = (v.flags & F_INFLIGHT) ? PH_POST : PH_DECIDE;
     }
+    if constexpr (TIMED) tm.lap(TM_TICK);
 #ifdef SFL_PROFILE
     {
       const uint64_t t1 = __builtin_amdgcn_s_memtime();
@@ -2272,6 +2357,11 @@ __device__ void run_groups(const SflMap& m, const SflState& s, const SflCtl& c) 
       phase = (v.flags & (F_TERM | F_TRUNC)) ? PH_END : PH_DECIDE;
       if (v.n_dec >= dec_budget) break;
     }
+    if constexpr (TIMED) {
+      tm.lap(TM_POST);
+      v.tm_on = tm.on;
+    }
+    const uint64_t dec_lanes = TIMED ? (uint64_t)__ballot(phase == PH_DECIDE) : 0ull;
 #ifdef SFL_PROFILE
     {
       const uint64_t t1 = __builtin_amdgcn_s_memtime();
@@ -2281,11 +2371,12 @@ __device__ void run_groups(const SflMap& m, const SflState& s, const SflCtl& c) 
 #endif
     if (phase == PH_DECIDE) {
       const bool greedy = (v.flags & F_GREEDY) != 0;
-      v.decide(d, greedy);
+      v.template decide<TIMED>(d, greedy);
       abytes += d.abytes;
       v.flags |= F_INFLIGHT;
       phase = many(v.q_mask) ? PH_POST : PH_TICK;
     }
+    if constexpr (TIMED) tm.decide_done(v, dec_lanes ? __builtin_ctzll(dec_lanes) : -1);
 #ifdef SFL_PROFILE
     gs[7] += __builtin_amdgcn_s_memtime() - tp0;
 #endif
@@ -2323,6 +2414,7 @@ __device__ void run_groups(const SflMap& m, const SflState& s, const SflCtl& c) 
     }
   }
   v.store(phase);
+  if constexpr (TIMED) tm.flush(c);
 #ifdef SFL_PROFILE
   {  // the counts of the group that left the loop last (it saw every iteration of the wave)
     uint64_t mx = gs[0];

@@ -60,9 +60,28 @@ class DistrQLearning:
         np.savez_compressed(os.path.join(out_dir, name), x=arr)
 
     def _timing(self, t0):
-        c = self.batch.counters()
-        self.env.step_time += time.time() - t0
-        self.env.flatland_step_time += c["last_kernel_ms"] * 1e-3
+        """The reference's accumulators (switch_env.py:67-73, distr_q.py:271-273, 304-358), from the device's
+        phase timers: flatland_step_time = the Flatland ticks, last_time = observe, action_selection_time =
+        epsilon-greedy, update_time = the post step (Q update, pending map, destination bonus), reset_time =
+        reset_total_time = the episode resets, step_time = apply + ticks (env.step incl. _move_trains_to_switch).
+        Without timers (the lane-per-env body) step_time is the call's wall time and flatland_step_time its
+        kernel time."""
+        ph = self.batch.phase_seconds()
+        prev = getattr(self, "_phase_prev", None) or {k: 0.0 for k in ph}
+        d = {k: ph[k] - prev[k] for k in ph}
+        self._phase_prev = ph
+        if sum(d.values()) > 0:
+            self.env.flatland_step_time += d["tick"]
+            self.env.last_time += d["observe"]
+            self.env.action_selection_time += d["egreedy"]
+            self.env.update_time += d["post"]
+            self.env.reset_time += d["reset"]
+            self.env.reset_total_time += d["reset"]
+            self.env.step_time += d["apply"] + d["tick"]
+        else:
+            c = self.batch.counters()
+            self.env.step_time += time.time() - t0
+            self.env.flatland_step_time += c["last_kernel_ms"] * 1e-3
 
     # ------------------------------------------------------------------
     def learn(self, num_episodes: int, out_dir: str, checkpoint_freq: int, exploit_freq: Optional[int] = None):

@@ -103,6 +103,7 @@ class Batch:
             self.lib.check(self.lib.dll.sfl_set_mf_schedule(self.h, tab.shape[1], _ptr(tab, C.c_uint8)),
                            "sfl_set_mf_schedule")
         self.learn_calls = 0
+        self.timed_kernel_ms = 0.0  # device time of the learn / test launches (the phase-timed ones)
         self.trace_env = None
         self.trace_cap = 1 << 16
         self.last_trace = None
@@ -165,6 +166,7 @@ class Batch:
             a.trace, a.trace_n = _ptr(tr, C.c_uint64), _ptr(tn, C.c_uint64)
             a.trace_env, a.trace_cap = int(self.trace_env), int(self.trace_cap)
         self.lib.check(fn(self.h, C.byref(a)), fn.__name__)
+        self.timed_kernel_ms += self.counters()["last_kernel_ms"]
         if tr is not None:
             self.last_trace = tr[:min(int(tn[0]), self.trace_cap)]
         for k in list(out):
@@ -198,6 +200,18 @@ class Batch:
         ms = C.c_double(0.0)
         self.lib.check(self.lib.dll.sfl_step(self.h, int(decisions_per_env), C.byref(n), C.byref(ms)), "sfl_step")
         return int(n.value), float(ms.value)
+
+    PHASES = ("tick", "observe", "egreedy", "apply", "post", "reset", "other")
+
+    def phase_seconds(self) -> Dict[str, float]:
+        """Device seconds per phase of the learn loop over this batch's learn / test launches so far: the
+        launches' kernel time split by the sampled in-kernel phase cycles (sfl_get_phase_cycles; all zero on the
+        lane-per-env body, which has no timers)."""
+        cyc = np.zeros(8, np.uint64)
+        self.lib.check(self.lib.dll.sfl_get_phase_cycles(self.h, _ptr(cyc, C.c_uint64), 8), "sfl_get_phase_cycles")
+        total = float(cyc[7])
+        sec = self.timed_kernel_ms * 1e-3
+        return {k: (sec * float(cyc[i]) / total if total > 0 else 0.0) for i, k in enumerate(self.PHASES)}
 
     def counters(self) -> dict:
         c = _lib.Counters()

@@ -40,5 +40,11 @@ if __name__ == "__main__":
     print("DONE!")
     print(f"TOTAL TIME: {elapsed_time:.1f} seconds")
     print(f"Seconds per episode: {elapsed_time / num_episodes:.1f}")
-    print(f"Device (kernel) time: {env.flatland_step_time:.3f} seconds")
-    print(f"Total step time: {env.step_time:.1f} seconds")
+    # the reference's timing breakdown (test_model.py:73-82), from the device's per-phase timers
+    print(f"Flatland step time: {env.flatland_step_time:.4f} seconds")
+    print(f"Total step time: {env.step_time:.4f} seconds")
+    print(f"Total last time: {env.last_time:.4f} seconds")
+    print(f"Action selection time: {env.action_selection_time:.4f} seconds")
+    print(f"Update time: {env.update_time:.4f} seconds")
+    print(f"Flatland reset time: {env.reset_time:.4f} seconds")
+    print(f"Total reset time: {env.reset_total_time:.4f} seconds")

@@ -534,3 +534,33 @@ def test_aec_batch_gpu_equals_host_build(lib, cfg):
     assert ends > 0 or cfg != "c2"
     bg.close()
     bh.close()
+
+
+def test_phase_timers_fill_the_reference_accumulators(lib, tmp_path):
+    """learn() runs the TIMED kernel: the seven accumulators of the reference's scripts
+    (switch_env.py:67-73, printed at test_model.py:73-82) are filled from the device's phase cycles, their
+    parts add up to the learn launches' kernel time, and the Q-tables equal an untimed run's (the trace
+    instantiation carries no timers): the timers only observe."""
+    env_mod = importlib.import_module("network-distributed-q-learning_amd.env")
+    dq = importlib.import_module("network-distributed-q-learning_amd.distr_q")
+    models = []
+    for traced in (False, True):
+        env = env_mod.ASyncSwitchEnv(mapgen.make_config("c3"), max_steps=100_000, n_envs=256)
+        model = dq.DistrQLearning(env=env, gamma=1.0, epsilon=0.5, epsilon_decay_rate=0.9997, lr=0.1,
+                                  lr_decay_rate=1.0, default_q=0.0, seed=450565, lib=lib)
+        assert model.batch.counters()["kernel_variant"] > 0
+        if traced:
+            model.batch.trace_env = 7
+        model.learn(num_episodes=2, out_dir=str(tmp_path), checkpoint_freq=10_000)
+        models.append((env, model))
+    env, model = models[0]
+    for k in ("flatland_step_time", "step_time", "last_time", "action_selection_time", "update_time",
+              "reset_time", "reset_total_time"):
+        assert getattr(env, k) > 0.0, k
+    ph = model.batch.phase_seconds()
+    assert abs(sum(ph.values()) - model.batch.timed_kernel_ms * 1e-3) <= 1e-6 * sum(ph.values())
+    assert sum(models[1][1].batch.phase_seconds().values()) == 0.0  # the traced run was untimed
+    for e in (0, 100, 255):
+        q0, t0 = model.batch.q_raw(e)
+        q1, t1 = models[1][1].batch.q_raw(e)
+        assert np.array_equal(q0, q1) and np.array_equal(t0, t1), e
