@@ -167,6 +167,17 @@ __global__ void __launch_bounds__(256) k_part_compact(const sfl::SflPart* __rest
     }
   }
   if (threadIdx.x == 0 && lmax) atomicMax(P->max_stage, lmax);
+  __syncthreads();  // (breq / bupd: this block's reservations)
+  // segment overflow of this round, known from the reservations: reported in this round's totals (before
+  // the last block hands them over), not in the next read
+  uint32_t ovf = 0;
+  if (valid && !dense) {
+    if (rd >= 0 && breq[rd] + kr >= P->cap_req) ovf = sfl::E_MSG_OVF;
+#pragma unroll
+    for (int i = 0; i < MAXU; ++i)
+      if ((uint32_t)i < nu && bupd[du[i]] + ku[i] >= P->cap_upd) ovf = sfl::E_MSG_OVF;
+  }
+  if (ovf) atomicOr((unsigned long long*)&P->sums[3], (unsigned long long)ovf);
   // the last block to get here writes the segment headers and hands the counts and totals to the
   // host copy (zeroing them for the next round): every block's reservations are done by then
   __shared__ bool last;
@@ -194,14 +205,11 @@ __global__ void __launch_bounds__(256) k_part_compact(const sfl::SflPart* __rest
     }
   }
   if (!valid || dense) return;
-  uint32_t ovf = 0;
   if (rd >= 0) {
     const uint32_t k = breq[rd] + kr;
     if (k < P->cap_req) {
       P->req_out[(size_t)rd * (P->cap_req + 1) + 1 + k] = P->req_st[e];
       P->req_ix[e] = ((uint32_t)rd << 24) | (1u + k);
-    } else {
-      ovf = sfl::E_MSG_OVF;
     }
   }
 #pragma unroll
@@ -209,13 +217,9 @@ __global__ void __launch_bounds__(256) k_part_compact(const sfl::SflPart* __rest
     if ((uint32_t)i < nu) {
       const uint32_t k = bupd[du[i]] + ku[i];
       if (k < P->cap_upd) P->upd_out[(size_t)du[i] * (P->cap_upd + 1) + 1 + k] = P->upd_st[(size_t)e * P->upd_env + i];
-      else ovf = sfl::E_MSG_OVF;
     }
   }
-  if (ovf) {
-    s->err[e] |= ovf;
-    atomicOr((unsigned long long*)&P->sums[3], (unsigned long long)ovf);
-  }
+  if (ovf) s->err[e] |= ovf;
 }
 __global__ void k_part_answer(const sfl::SflMap* __restrict__ m, const sfl::SflPart* __restrict__ P,
                               const sfl::PartReq* __restrict__ in, sfl::PartRep* __restrict__ out) {

@@ -1418,8 +1418,6 @@ SFL_FN void env_run_ext(const SflMap& m, const SflState& s, const SflCtl& c, uin
       if (s.step_ctr[e] > m.max_steps) v.flags |= F_TRUNC;
       phase = (v.flags & (F_TERM | F_TRUNC)) ? PH_END : PH_DECIDE;
     } else {  // PH_END: report the episode (the learner records arrivals, delays, malfunctions)
-      for (int h = 0; h < m.T; ++h) x.delays[(size_t)h * s.E + e] = s.tr_delay[v.ix(h)];
-      x.n_mf[e] = s.n_mf[e];
       x.truncated[e] = (v.flags & F_TRUNC) ? 1 : 0;
       x.agent[e] = -1;
       v.flags &= ~F_EXT_OBS;
@@ -1427,6 +1425,10 @@ SFL_FN void env_run_ext(const SflMap& m, const SflState& s, const SflCtl& c, uin
       break;
     }
   }
+  // the episode's delays and malfunction count as they stand (its final values when agent == -1)
+  for (int h = 0; h < m.T; ++h) x.delays[(size_t)h * s.E + e] = s.tr_delay[v.ix(h)];
+  x.n_mf[e] = s.n_mf[e];
+  if (x.agent[e] >= 0) x.truncated[e] = 0;
 #pragma unroll
   for (int w = 0; w < MAXW; ++w) x.arrived[(size_t)w * s.E + e] = w < NW ? v.msk[1][w < NW ? w : 0] : 0u;
   v.masks_store();
