@@ -37,6 +37,12 @@ namespace wave {
 #ifndef SFL_PF_RING64
 #define SFL_PF_RING64 16  // one env per wavefront with two train slots per lane (c5, k_wave2): see WEnv::RING
 #endif
+#ifndef SFL_LATE_STORES
+// run_groups: the post step's global writes are buffered in LDS and issued at the end of the loop
+// iteration, after the next decision's loads (vmcnt counts stores too: a load issued after them waits for
+// their acknowledgements); a load that may read a buffered address flushes first (see flush_stores)
+#define SFL_LATE_STORES 0
+#endif
 #ifndef SFL_TICK_HOLD
 #define SFL_TICK_HOLD 2  // run_groups: ticks wait while this many groups of the wave can still decide
 #endif
@@ -68,7 +74,13 @@ constexpr uint32_t PF_NONE = 0xFFFFFFFFu;
 // (reward of STOP), if it moves with final rail action 1..3 (reward of a route), and the row's
 // argmax | first allowed argmax << 8 under the staged observation (the row's columns themselves are
 // not kept: a decision on a staged row needs only its max and argmaxes)
+#ifdef SFL_EPS_STAGE
+// doubles and 32-bit words of a prefetch record (stored apart: [TW][PF_D] and [TW][PF_WI]); double 3: the
+// decision's epsilon, staged for its switch's count at the prefetch (-1: none)
+constexpr int PF_D = 4, PF_WI = 3;
+#else
 constexpr int PF_D = 3, PF_WI = 3;  // doubles and 32-bit words of a prefetch record (stored apart: [TW][3] each)
+#endif
 constexpr int PF_WORDS = 2 * PF_D + PF_WI;
 // (doubles: pending cell value, slot word, row max; words: 0 distance at the cell | along the STOP
 // plan << 16, 1 route final action 1 | 2 << 16, 2 route final action 3 | argmax pack << 16 (int16
@@ -300,6 +312,7 @@ struct WEnv {
   // G < 64: the block's LDS copies of the per-switch and per-port map records (sw_pack [S][16],
   // port_pack and port_tr [4S][4]); G = 64 reads them with scalar loads
   const uint32_t* tsw = nullptr;
+  static constexpr int SW_LDS = 12;  // words of a switch record in the block's LDS copy (10 used of sw_pack's 16)
   const uint32_t* tpp = nullptr;
   const uint32_t* tpt = nullptr;
   // this env's semaphore records and switch counters in LDS (one region per wave):
@@ -327,6 +340,10 @@ struct WEnv {
   // the epsilon-greedy stream (numpy PCG64 state, increment, buffered half) lives in LDS: it is
   // touched once per decision and would otherwise hold ten registers across the whole loop
   uint64_t* lrng;  // [6]: state hi, lo, inc hi, lo, has << 32 | buf
+  // SFL_LATE_STORES (G < 64): the post step's buffered global writes -- u64 values [3] (Q cell, slot words),
+  // u32 offsets [5] (Q cell, slot A, slot B, key-set rows pend / cur), u32 valid bits
+  static constexpr bool LATE = SFL_LATE_STORES && G < 64 && !PART;
+  uint32_t* lsb = nullptr;
   int64_t cum;     // cumulative reward: a sum of integer rewards, exact in f64 (converted on store)
   int32_t n_mf, ep_dec, ep_ticks;
   int32_t step_ctr;
@@ -360,6 +377,7 @@ struct WEnv {
     }
     lpi = (uint32_t*)(lpf + PF_SLOTS * PF_D);
     lrng = (uint64_t*)(lds + G * (PPL + SPL) + PF_SLOTS * PF_WORDS);
+    if constexpr (LATE) lsb = lds + G * (PPL + SPL) + PF_SLOTS * PF_WORDS + 12;
     // PART: the timetable rows are read from the map (L2-resident): a launch runs one or two
     // decisions, so a per-launch LDS copy would cost more than it saves
     if constexpr (PART) ltt = m.tr_pack;
@@ -502,12 +520,12 @@ struct WEnv {
   // ---- map records --------------------------------------------------------------------
   __device__ __forceinline__ SwRec sw_rec(int sw) const {
     if constexpr (G == 64) return SwRec{LDCV<u8>(m.sw_pack, (size_t)sw * 2u)};
-    else return SwRec{*(const u8*)(tsw + 16 * sw)};
+    else return SwRec{*(const u8*)(tsw + SW_LDS * sw)};
   }
   // neighbour ports of the switch's ports 0-3 (16 bits each)
   __device__ __forceinline__ vec_t<uint32_t, 2> sw_nb(int sw) const {
     if constexpr (G == 64) return LDCV<vec_t<uint32_t, 2>>(m.sw_pack, (size_t)sw * 8u + 4u);
-    else return *(const vec_t<uint32_t, 2>*)(tsw + 16 * sw + 8);
+    else return *(const vec_t<uint32_t, 2>*)(tsw + SW_LDS * sw + 8);
   }
   __device__ __forceinline__ PortRec port_rec(int p) const {
     if constexpr (G == 64) return PortRec{LDCV<u4>(m.port_pack, (size_t)p)};
@@ -521,11 +539,11 @@ struct WEnv {
   // lane-parallel (per-lane index) reads of the same records: vector loads for G = 64, LDS else
   __device__ __forceinline__ u4 sw_v4(int sw, int q) const {
     if constexpr (G == 64) return ld((const u4*)m.sw_pack, (size_t)sw * 4u + (uint32_t)q);
-    else return *(const u4*)(tsw + 16 * sw + 4 * q);
+    else return *(const u4*)(tsw + SW_LDS * sw + 4 * q);
   }
   __device__ __forceinline__ vec_t<uint32_t, 2> sw_nb_v(int sw) const {
     if constexpr (G == 64) return ld((const vec_t<uint32_t, 2>*)m.sw_pack, (size_t)sw * 8u + 4u);
-    else return *(const vec_t<uint32_t, 2>*)(tsw + 16 * sw + 8);
+    else return *(const vec_t<uint32_t, 2>*)(tsw + SW_LDS * sw + 8);
   }
   __device__ __forceinline__ u4 port_v(int p) const {
     if constexpr (G == 64) return ld((const u4*)m.port_pack, (size_t)p);
@@ -1205,7 +1223,24 @@ struct WEnv {
   // (after the batch's earlier decisions changed the semaphores) is the staged one, and staged
   // Q values are dropped when the batch writes their cell (pf_written).  Slot words are never
   // stale: a decision writes only its own train's slots and a train decides once per batch.
+  // issue the buffered writes of the last post step (LATE): lanes 0-2 the 8-byte stores, lanes 3-4 the
+  // key-set inserts, one instruction each
+  __device__ __forceinline__ void flush_stores() {
+    if constexpr (LATE) {
+      const uint32_t vm = lsb[11];
+      if (vm) {
+        const int l = lid();
+        const uint32_t off = lsb[6 + (l < 5 ? l : 0)];
+        const uint64_t val = ((const uint64_t*)lsb)[l < 3 ? l : 0];
+        const bool on = l < 5 && ((vm >> l) & 1u);
+        if (on && l < 3) st(l == 0 ? (uint64_t*)qbase() : sbase(), (size_t)off, val);
+        if (on && l >= 3) touch_row(off);
+        lsb[11] = 0u;  // uniform value from every lane
+      }
+    }
+  }
   __device__ __forceinline__ void prefetch(bool greedy) {
+    flush_stores();  // (the staging reads slot words and Q cells the buffered writes may hit)
     const Mask malf = malf_mask();
 #pragma unroll
     for (int k = 0; k < TPL; ++k) pf_roff[k] = pf_qoff[k] = PF_NONE;
@@ -1215,6 +1250,9 @@ struct WEnv {
     // does not survive the launch): stage that train only
     const int h_first = PART ? mctz(q_mask) : -1;
     pf_n = 0;
+#ifdef SFL_EPS_STAGE
+    lrng[5] = 0ull;  // switches decided on since this staging (their staged epsilons are stale)
+#endif
 #pragma unroll 1
     for (int k = 0; k < TPL; ++k) {
       if (!mbit(q_mask, lid() + G * k)) continue;
@@ -1266,6 +1304,13 @@ struct WEnv {
     const vec_t<uint32_t, 2> nbw = sw_nb_v(sw);
     const vec_t<int32_t, 4> trw = *(const vec_t<int32_t, 4>*)(ltt + 8 * hk);  // ed, la, k, target
     const u4 pr = port_v(4 * sw + slot);
+#ifdef SFL_EPS_STAGE
+    // epsilon of the decision for its switch's count as it stands (distr_q.py:59-68), a level-1 load; the
+    // decision uses it unless an earlier decision since the staging was on the same switch (lrng[5])
+    const uint32_t n_sw = cget_var(sw);
+    const double eps_h = (greedy || PART || n_sw >= (uint32_t)m.ntab) ? -1.0
+                         : (xp::kEpsConst ? m.eps0 : ld(m.eps_tab, (size_t)(n_sw < (uint32_t)m.ntab ? n_sw : 0u)));
+#endif
     const uint32_t n_plan = pl_len(plan_k);
     const uint32_t a1 = n_plan ? pl_front(plan_k) : A_FWD;
     // move-table rows (all four rail actions) at the cell and after the first rail action
@@ -1378,6 +1423,9 @@ struct WEnv {
     }
     pfl[0] = qv;
     pfl[1] = __longlong_as_double((long long)slw);
+#ifdef SFL_EPS_STAGE
+    pfl[3] = eps_h;
+#endif
     pfi[0] = d16(dd) | (d16(d_stop) << 16);
     pfi[1] = d16(d_rt[1]) | (d16(d_rt[2]) << 16);
     roff_out = (row_ok && !PART) ? roff : PF_NONE;
@@ -1507,6 +1555,7 @@ struct WEnv {
     if (row_hit) {
       SFL_PCNT(4);
     } else if (loc) {
+      flush_stores();
       v_c = ld(qbase() + roff, (size_t)(colv ? lid() : 0));
       SFL_PCNT(5);
     }
@@ -1529,6 +1578,7 @@ struct WEnv {
         q_pend_v = pf_qp;
         SFL_PCNT(6);
       } else {
+        flush_stores();
         q_pend_v = ld(qbase(), (size_t)d.qoff_pend);
         SFL_PCNT(7);
       }
@@ -1550,8 +1600,19 @@ struct WEnv {
       rng.buf = (uint32_t)rng_w[4];
       const uint32_t n = n_sw;
       // eps0 * decay**n (distr_q.py:59-68): host-computed table (a scalar load, K$-resident), pow beyond it
+#ifdef SFL_EPS_STAGE
+      // (read here, not with the decision's first LDS reads: held across the observation they spilled)
+      const double eps_st = pfh[3];
+      const uint64_t eps_dirty = lrng[5];
+      const bool st_ok = !PART && Ud(eps_st) >= 0.0 && !((U(eps_dirty) >> (sw & 63)) & 1ull);
+      if (!PART && !observe_only) lrng[5] = eps_dirty | (1ull << (sw & 63));  // uniform value from every lane
+      const double eps = st_ok ? Ud(eps_st)
+                         : xp::kEpsConst ? m.eps0
+                         : n < (uint32_t)m.ntab ? LDC(m.eps_tab, (size_t)n) : m.eps0 * pow_ool(m.eps_decay, (double)n);
+#else
       const double eps = xp::kEpsConst ? m.eps0
                          : n < (uint32_t)m.ntab ? LDC(m.eps_tab, (size_t)n) : m.eps0 * pow_ool(m.eps_decay, (double)n);
+#endif
       explore = Ud(pcg_double(rng)) < eps;
       if (explore && !observe_only) {
         const uint32_t sub_seed = pcg_bounded(rng, 2147483646u);
@@ -1818,6 +1879,34 @@ struct WEnv {
     }
     // every global write of the step from one lane-0 region
     // (xp::kNo*: timing-only experiment builds that drop one class of store, sfl_experiment.h)
+    if constexpr (LATE && !xp::kNoQStore && !xp::kNoTouch && !xp::kNoSlot) {
+      // buffered (flush_stores): uniform values, written by every lane
+      ((uint64_t*)lsb)[0] = (uint64_t)__double_as_longlong(nv);
+      ((uint64_t*)lsb)[1] = slot_make(PEND_NONE, slot_rew(d.slotword, epoch), epoch);
+      ((uint64_t*)lsb)[2] = slot_make(pend_make((uint32_t)d.sw, (uint32_t)d.slot, d.state, (uint32_t)d.j), d.r_new, epoch);
+      lsb[6] = d.qoff_pend;
+      lsb[7] = slot_ix(d.sw, d.h);
+      lsb[8] = slot_ix(d.next_sw, d.h);
+      lsb[9] = d.row_pend;
+      lsb[10] = d.row_cur;
+      // (slot B replaces slot A when the train stays at its switch: one lane per address)
+      lsb[11] = (hp ? 9u : 0u) | ((hp && d.next_sw != d.sw) ? 2u : 0u) | 4u | ((d.touch_cur || (hp && d.sw != ps)) ? 16u : 0u);
+    } else
+#ifdef SFL_POST_LANES
+    // the step's global writes as two instructions over five lanes of the group: lanes 0-2 the 8-byte
+    // stores (the pending update's Q cell, the two slot words), lanes 3-4 the key-set inserts
+    if constexpr (!xp::kNoQStore && !xp::kNoTouch && !xp::kNoSlot) {
+      const int l = lid();
+      const uint64_t sa = slot_make(PEND_NONE, slot_rew(d.slotword, epoch), epoch);
+      const uint64_t sb = slot_make(pend_make((uint32_t)d.sw, (uint32_t)d.slot, d.state, (uint32_t)d.j), d.r_new, epoch);
+      const size_t off = l == 0 ? (size_t)d.qoff_pend : (size_t)slot_ix(l == 1 ? d.sw : d.next_sw, d.h);
+      uint64_t* base = l == 0 ? (uint64_t*)qbase() : sbase();
+      const uint64_t val = l == 0 ? (uint64_t)__double_as_longlong(nv) : (l == 1 ? sa : sb);
+      if ((l == 0 && hp) || l == 1 || l == 2) st(base, off, val);
+      const bool ins = (l == 3 && hp) || (l == 4 && (d.touch_cur || (hp && d.sw != ps)));
+      if (ins) touch_row(l == 3 ? d.row_pend : d.row_cur);
+    } else
+#endif
     if (lid() == 0) {
       if (hp) {
         if (!xp::kNoQStore) st(qbase(), (size_t)d.qoff_pend, nv);
@@ -1836,7 +1925,10 @@ struct WEnv {
     // same successor switch => same slot), so the lanes' updates are independent.
     Mask fresh = arr_mask & ~fl_mask;
     fl_mask |= fresh;
-    if (many(fresh)) pf_ok = false;  // bonus writes: stage the rest of the batch again
+    if (many(fresh)) {
+      pf_ok = false;  // bonus writes: stage the rest of the batch again
+      flush_stores();  // (the bonus reads slot words and Q cells the buffered writes may hit)
+    }
     while (many(fresh)) {
       const int tr = mctz(fresh);
       mclear_low(fresh);
@@ -2228,12 +2320,13 @@ __device__ void run_groups(const SflMap& m, const SflState& s, const SflCtl& c) 
   // per env: semaphores, counters, prefetch records, rng; per block: the timetable rows and the
   // per-switch / per-port map records (the groups of a wave read different switches' records: LDS
   // reads instead of vector loads)
-  constexpr int LDS_WORDS = (G * (PPL + SPL) + V::PF_SLOTS * PF_WORDS + 12 + 3) / 4 * 4;
+  constexpr int LDS_WORDS = (G * (PPL + SPL) + V::PF_SLOTS * PF_WORDS + 12 + (V::LATE ? 12 : 0) + 3) / 4 * 4;
   constexpr int EPB = SFL_WAVE_BLOCK / G;  // envs per block (sfl.hip launches)
   constexpr int SWX = G * SPL, NPX = G * PPL;  // switches / ports the shape holds
-  constexpr int O_TT = EPB * LDS_WORDS, O_SW = O_TT + TW * 8, O_PP = O_SW + SWX * 16, O_PT = O_PP + NPX * 4;
+  constexpr int O_TT = EPB * LDS_WORDS, O_SW = O_TT + TW * 8, O_PP = O_SW + SWX * V::SW_LDS, O_PT = O_PP + NPX * 4;
   __shared__ __attribute__((aligned(16))) uint32_t lds[O_PT + NPX * 4];
-  for (int i = (int)threadIdx.x; i < m.S * 16; i += (int)blockDim.x) lds[O_SW + i] = m.sw_pack[i];
+  for (int i = (int)threadIdx.x; i < m.S * V::SW_LDS; i += (int)blockDim.x)
+    lds[O_SW + i] = m.sw_pack[(i / V::SW_LDS) * 16 + i % V::SW_LDS];
   for (int i = (int)threadIdx.x; i < m.NP * 4; i += (int)blockDim.x) {
     lds[O_PP + i] = m.port_pack[i];
     lds[O_PT + i] = m.port_tr[i];
@@ -2247,6 +2340,7 @@ __device__ void run_groups(const SflMap& m, const SflState& s, const SflCtl& c) 
   v.tpt = lds + O_PT;
   PhaseTimer tm;
   if constexpr (TIMED) tm.start(c.phase_cyc != nullptr && blockIdx.x % TM_SAMPLE == 0u && threadIdx.x < 64u);
+  if constexpr (V::LATE) v.lsb[11] = 0u;
   v.load();
   int32_t phase = ld(s.phase, e);
   int32_t ep_t = ld(s.ep_t, e), n_test = ld(s.n_test, e);
@@ -2412,7 +2506,9 @@ __device__ void run_groups(const SflMap& m, const SflState& s, const SflCtl& c) 
       }
       phase = PH_RESET;
     }
+    v.flush_stores();  // LATE: the iteration's post writes, after its decision's loads
   }
+  v.flush_stores();
   v.store(phase);
   if constexpr (TIMED) tm.flush(c);
 #ifdef SFL_PROFILE

@@ -7,7 +7,7 @@ OUT=gpurun_out/${TAG:-ab}
 mkdir -p $OUT
 for L in ${LIBS:-libsfl}; do
   export SFL_LIB=$GRAFT_REPO_ROOT/network-distributed-q-learning_amd/$L.so
-  V="--verify-envs 0 --experimental"; [ "$L" = "libsfl" ] && V=""
+  V="--verify-envs ${VERIFY_ENVS:-0} --experimental"; [ "$L" = "libsfl" ] && V=""
   timeout -k 10 300 python bench.py --steps ${STEPS:-10} --warmup 2 --no-cpu $V ${BENCH_ARGS} > $OUT/${L}.json 2> $OUT/${L}.err; rc=$?; echo "$L bench rc=$rc"; [ $rc -eq 0 ] || exit $rc
   python -c "import json;d=json.load(open('$OUT/${L}.json'));print('  %.1fM/s kernel %.3f ms parity %s' % (d['value']/1e6, d['roofline']['avg_kernel_ms'], d.get('parity')))"
   if [ -n "$PMC" ]; then
