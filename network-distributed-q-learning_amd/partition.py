@@ -284,14 +284,16 @@ class PartitionedBatch:
         ptr = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
         self.lib.check(d.sfl_part_begin(h), "sfl_part_begin")
         sized = self._sized()
-        # one rank on the GPU with every row sent as a message: the decisions+1 rounds queue on the
-        # stream without a synchronisation; the counts (open requests, the envs' errors) are read
-        # after the last one.  Otherwise each round's counts end the step as soon as no request is
-        # open anywhere (with local rows one rank needs a single round)
-        deferred = self.stream is not None and not sized and not self.local_rows
+        # one rank on the GPU: the rounds queue on the stream without a synchronisation, and the counts
+        # (open requests, the envs' errors) are read only after rounds 1, 2, 4, ..., 32 and then every
+        # 32nd (with every row in place one round is the whole step; with messages the step runs its
+        # decisions + 1 rounds, the last few possibly empty).  Otherwise (N > 1 ranks, or the host
+        # build) each round's counts end the step as soon as no request is open anywhere
+        deferred = self.stream is not None and not sized
         rounds = 0
         n_open = 0
-        for _ in range(int(decisions_per_env) + 1):
+        last = int(decisions_per_env) + 1
+        for _ in range(last):
             n = C.c_uint64(0)
             # a failure on one rank (error flags of its envs, message overflow) must stop every rank,
             # or the others would wait forever in the next exchange: the flag travels with the counts
@@ -319,13 +321,16 @@ class PartitionedBatch:
             else:
                 self._exchange(self.rep_recv, self.rep_send)
             rounds += 1
-            if not deferred and n_open == 0:
+            if deferred and (rounds & (rounds - 1) == 0 and rounds <= 32 or rounds % 32 == 0 or rounds == last):
+                counts = self._local_counts()
+                if counts is None:
+                    raise _lib.SflError(f"rank {self.rank}: sfl_part_local: " +
+                                        d.sfl_last_error().decode(errors="replace"))
+                n_open = sum(counts[0])
+                if n_open == 0:
+                    break
+            elif not deferred and n_open == 0:
                 break  # every env has made its decisions (this round's updates are applied)
-        if deferred:
-            counts = self._local_counts()
-            if counts is None:
-                raise _lib.SflError(f"rank {self.rank}: sfl_part_local: " + d.sfl_last_error().decode(errors="replace"))
-            n_open = sum(counts[0])
         if (not sized) and self._any_rank(1 if n_open != 0 else 0) or sized and n_open != 0:
             raise _lib.SflError(f"rank {self.rank}: requests still open after the last round "
                                 f"({n_open} on this rank)")
