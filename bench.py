@@ -188,7 +188,7 @@ def parity_field(dist, n_checked: int, bad, device=None):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--decisions", type=int, default=1024, help="agent-env-steps per env per step (one launch)")
     ap.add_argument("--envs", type=int, default=65536, help="envs per GPU")

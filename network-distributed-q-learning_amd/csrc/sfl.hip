@@ -61,7 +61,7 @@ __global__ void __launch_bounds__(SFL_WAVE_BLOCK) __attribute__((amdgpu_waves_pe
 #define SFL_GROUP_OCC (SFL_PF_RING > 0 ? 4 : 3)  // two slots per lane: 4 with the prefetch ring (LDS 4 blocks/CU)
 #endif
 template <int PPL, int SPL, int TW, bool TRACE, int G, bool TIMED = false>
-__global__ void __launch_bounds__(SFL_WAVE_BLOCK) __attribute__((amdgpu_waves_per_eu(TW <= G ? SFL_GROUP_OCC1 : SFL_GROUP_OCC)))
+__global__ void __launch_bounds__(SFL_GROUP_BLOCK) __attribute__((amdgpu_waves_per_eu(TW <= G ? SFL_GROUP_OCC1 : SFL_GROUP_OCC)))
 k_wave_g(const sfl::SflMap* __restrict__ m, const sfl::SflState* __restrict__ s, const sfl::SflCtl* __restrict__ c) {
   sfl::wave::run_groups<PPL, SPL, TW, TRACE, G, TIMED>(*m, *s, *c);
 }
@@ -475,10 +475,10 @@ struct HipBackend {
 #define SFL_KG(v)                                                                                               \
   {                                                                                                             \
     constexpr sfl::WaveShape w = sfl::kVariants[v];                                                             \
-    const unsigned gblocks = (unsigned)(((size_t)s.E * w.G + SFL_WAVE_BLOCK - 1) / SFL_WAVE_BLOCK);             \
-    if (c.trace) k_wave_g<w.PPL, w.SPL, w.TW, true, w.G><<<gblocks, SFL_WAVE_BLOCK, 0, stream>>>(pm, ps, pc);    \
-    else if (c.phase_cyc) k_wave_g<w.PPL, w.SPL, w.TW, false, w.G, true><<<gblocks, SFL_WAVE_BLOCK, 0, stream>>>(pm, ps, pc); \
-    else k_wave_g<w.PPL, w.SPL, w.TW, false, w.G><<<gblocks, SFL_WAVE_BLOCK, 0, stream>>>(pm, ps, pc);          \
+    const unsigned gblocks = (unsigned)(((size_t)s.E * w.G + SFL_GROUP_BLOCK - 1) / SFL_GROUP_BLOCK);             \
+    if (c.trace) k_wave_g<w.PPL, w.SPL, w.TW, true, w.G><<<gblocks, SFL_GROUP_BLOCK, 0, stream>>>(pm, ps, pc);    \
+    else if (c.phase_cyc) k_wave_g<w.PPL, w.SPL, w.TW, false, w.G, true><<<gblocks, SFL_GROUP_BLOCK, 0, stream>>>(pm, ps, pc); \
+    else k_wave_g<w.PPL, w.SPL, w.TW, false, w.G><<<gblocks, SFL_GROUP_BLOCK, 0, stream>>>(pm, ps, pc);          \
   }
     static_assert(sfl::kVariants[5].TW > 64 && sfl::kNumVariants == 10, "variant 5 is the two-slot shape, 6-9 grouped");
     if (variant == 1) SFL_KW(1)

@@ -46,6 +46,9 @@ namespace wave {
 #ifndef SFL_TICK_HOLD
 #define SFL_TICK_HOLD 2  // run_groups: ticks wait while this many groups of the wave can still decide
 #endif
+#ifndef SFL_TICK_REMMIN
+#define SFL_TICK_REMMIN 5  // ... and one of them has fewer than this many decisions left (0: hold regardless)
+#endif
 #ifdef SFL_PROFILE
 // tuning builds only: wall cycles per phase summed over waves (reset, tick, decide, post, total,
 // decide = observe + egreedy + apply)
@@ -98,6 +101,9 @@ __device__ __forceinline__ int32_t d16_lo(uint32_t w) {
 __device__ __forceinline__ int32_t d16_hi(uint32_t w) { return d16_lo(w >> 16); }
 #ifndef SFL_WAVE_BLOCK
 #define SFL_WAVE_BLOCK 256  // threads per k_wave block (envs per block x 64)
+#endif
+#ifndef SFL_GROUP_BLOCK
+#define SFL_GROUP_BLOCK SFL_WAVE_BLOCK  // threads per k_wave_g block (run_groups: envs per block x G)
 #endif
 constexpr int32_t PF_OFFGRID = (int32_t)0x80000000;  // projection left the grid
 
@@ -1253,7 +1259,11 @@ struct WEnv {
 #ifdef SFL_EPS_STAGE
     lrng[5] = 0ull;  // switches decided on since this staging (their staged epsilons are stale)
 #endif
+#ifdef SFL_PF_UNROLL
+#pragma unroll
+#else
 #pragma unroll 1
+#endif
     for (int k = 0; k < TPL; ++k) {
       if (!mbit(q_mask, lid() + G * k)) continue;
       if (PART && lid() + G * k != h_first) continue;
@@ -2321,7 +2331,7 @@ __device__ void run_groups(const SflMap& m, const SflState& s, const SflCtl& c) 
   // per-switch / per-port map records (the groups of a wave read different switches' records: LDS
   // reads instead of vector loads)
   constexpr int LDS_WORDS = (G * (PPL + SPL) + V::PF_SLOTS * PF_WORDS + 12 + (V::LATE ? 12 : 0) + 3) / 4 * 4;
-  constexpr int EPB = SFL_WAVE_BLOCK / G;  // envs per block (sfl.hip launches)
+  constexpr int EPB = SFL_GROUP_BLOCK / G;  // envs per block (sfl.hip launches)
   constexpr int SWX = G * SPL, NPX = G * PPL;  // switches / ports the shape holds
   constexpr int O_TT = EPB * LDS_WORDS, O_SW = O_TT + TW * 8, O_PP = O_SW + SWX * V::SW_LDS, O_PT = O_PP + NPX * 4;
   __shared__ __attribute__((aligned(16))) uint32_t lds[O_PT + NPX * 4];
@@ -2400,8 +2410,15 @@ __device__ void run_groups(const SflMap& m, const SflState& s, const SflCtl& c) 
     // batch alongside.  Measured at G = 16 (c3): hold while >= 2 decide 1,316 M, while >= 1
     // (ticks only when no group decides) 1,263 M, tick as soon as 3 / 2 groups wait 1,308 / 1,245 M,
     // never hold 14 % below the second.
-    const bool wave_decides =
-        (int)__builtin_popcountll(__ballot(phase == PH_POST || phase == PH_DECIDE)) >= SFL_TICK_HOLD * G;
+    // Round 3: they also tick while every deciding group still has at least SFL_TICK_REMMIN decisions
+    // left in its batch -- the ticking groups then decide alongside it instead of idling to its end.
+    // scripts/sched_model.py replays c3 decision streams through this loop and prices the blocks an
+    // iteration executes (profiles/r03_sched_model.txt): the rule is worth ~1.6 % there, measured
+    // +0.65 % / +1.0 % on two boxes (profiles/r03_ab_sched.txt); aligning the groups perfectly would
+    // give at most 28 %, and no rule tried gets more than the 1.6 %.
+    const bool dec_ph = phase == PH_POST || phase == PH_DECIDE;
+    const bool wave_decides = (int)__builtin_popcountll(__ballot(dec_ph)) >= SFL_TICK_HOLD * G &&
+                              (SFL_TICK_REMMIN <= 0 || __ballot(dec_ph && mpopc(v.q_mask) < SFL_TICK_REMMIN) != 0ull);
 #else
     const bool wave_decides = false;
 #endif

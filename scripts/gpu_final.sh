@@ -7,7 +7,7 @@ OUT=gpurun_out/${TAG:-final}
 mkdir -p $OUT
 timeout -k 10 300 python __graft_entry__.py > $OUT/smoke.log 2>&1; rc=$?; echo "smoke rc=$rc"; tail -1 $OUT/smoke.log
 [ $rc -eq 0 ] || exit $rc
-timeout -k 10 600 python bench.py --steps 10 --warmup 2 > $OUT/bench.json 2> $OUT/bench.err; rc=$?; echo "bench rc=$rc"
+timeout -k 10 600 python bench.py > $OUT/bench.json 2> $OUT/bench.err; rc=$?; echo "bench rc=$rc"
 [ $rc -eq 0 ] || { tail -5 $OUT/bench.err; exit $rc; }
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o ktrace --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu --verify-envs 0 > $OUT/prof_bench.json 2>/dev/null; rc=$?; echo "ktrace rc=$rc"; [ $rc -eq 0 ] || exit $rc
 for C in FETCH_SIZE WRITE_SIZE "TCC_HIT_sum TCC_MISS_sum"; do
