@@ -34,7 +34,8 @@ def main(path, sub="k_wave_g"):
         if sub not in name:
             continue
         g = lambda k: re.search(r"\." + k + r":\s+(\d+)", blk).group(1)
-        print(f"{name[:90]:90s} vgpr {g('vgpr_count'):>3s} vspill {g('vgpr_spill_count'):>3s} "
+        agpr = blk.split()[0]
+        print(f"{name[:90]:90s} agpr {agpr:>3s} vgpr {g('vgpr_count'):>3s} vspill {g('vgpr_spill_count'):>3s} "
               f"sspill {g('sgpr_spill_count'):>3s} lds {g('group_segment_fixed_size'):>6s} "
               f"scratch {g('private_segment_fixed_size'):>4s}")
 
