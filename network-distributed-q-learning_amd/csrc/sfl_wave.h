@@ -46,6 +46,9 @@ namespace wave {
 #ifndef SFL_TICK_HOLD
 #define SFL_TICK_HOLD 2  // run_groups: ticks wait while this many groups of the wave can still decide
 #endif
+#ifndef SFL_LOAD_BATCH
+#define SFL_LOAD_BATCH 1  // WEnv::load issues every state load before using any (0: per-record conditional loads)
+#endif
 #ifndef SFL_TICK_REMMIN
 #define SFL_TICK_REMMIN 5  // ... and one of them has fewer than this many decisions left (0: hold regardless)
 #endif
@@ -358,7 +361,10 @@ struct WEnv {
   int32_t req_dst_v = -1;  // destination of the request (-1: none)
   uint32_t n_upd = 0;      // update records staged
   uint32_t stg = 0;        // next update stage of this launch (the posts' records in program order)
-  uint32_t sem0[PART ? PPL : 1], cnt0[PART ? SPL : 1];  // the launch's loaded records / counters
+  // PART: the launch's loaded semaphore records and counters, [64 * (PPL + SPL)] words of the env's LDS region
+  // (store() writes back only what changed).  Held in registers they were spilled, and every conditional
+  // store of the write-back then waited for its predecessors (a scratch reload's vmcnt counts stores too)
+  uint32_t* lsem0 = nullptr;
   // product phase timers (the TIMED kernels that learn() / test() run; sfl_get_phase_cycles): decide<true>
   // stamps the end of its observe and epsilon-greedy sections on a sampled wavefront (tm_on); run_groups
   // reads the stamps from a deciding lane after the (divergent) decide block
@@ -740,6 +746,64 @@ struct WEnv {
 
   // ---- launch-boundary state transfer ---------------------------------------------------------
   __device__ __forceinline__ void load() {
+#if SFL_LOAD_BATCH
+    // every per-lane load is issued unconditionally (clamped index) before any result is used: as conditional
+    // loads each sat in its own exec-masked block and waited for its own HBM round trip (16 + 4 + 2 x 8 in a
+    // row for c5's partitioned local step, which loads the state every round)
+    uint32_t tw[TPL][8];
+#pragma unroll
+    for (int k = 0; k < TPL; ++k) {
+      const size_t ti = tix(mine[k] ? lane + G * k : 0);
+      tw[k][0] = (uint32_t)ld(s.tr_pos, ti);
+      tw[k][1] = ld(s.tr_bits, ti);
+      tw[k][2] = ld(s.tr_plan, ti);
+      tw[k][3] = ld(s.tr_next, ti);
+      tw[k][4] = ld(s.tr_prev, ti);
+      tw[k][5] = ld(s.tr_src, ti);
+      tw[k][6] = ld(s.tr_dec, ti);
+      tw[k][7] = (uint32_t)ld(s.tr_delay, ti);
+    }
+    uint32_t rw[PPL], nw[SPL];
+#pragma unroll
+    for (int k = 0; k < PPL; ++k) rw[k] = ld(sem_words(), pix(k * G + lane < m.NP ? k * G + lane : 0));
+#pragma unroll
+    for (int k = 0; k < SPL; ++k) nw[k] = ld(s.counts, cix(k * G + lane < m.S ? k * G + lane : 0));
+#pragma unroll
+    for (int k = 0; k < TPL; ++k) {
+      const int hk = lane + G * k;
+      if (mine[k]) {
+        pos[k] = (int32_t)tw[k][0];
+        bits[k] = tw[k][1];
+        plan[k] = tw[k][2];
+        nprv[k] = tw[k][3] | (tw[k][4] << 16);
+        sdec[k] = tw[k][5] | (tw[k][6] << 16);
+        delay[k] = (int32_t)tw[k][7];
+        if constexpr (!PART) {
+          *(vec_t<int32_t, 4>*)(ltt + 8 * hk) = ld((const vec_t<int32_t, 4>*)m.tr_pack, (size_t)hk * 2u);
+          *(vec_t<int32_t, 4>*)(ltt + 8 * hk + 4) = ld((const vec_t<int32_t, 4>*)m.tr_pack, (size_t)hk * 2u + 1u);
+        }
+      } else {
+        pos[k] = -1;
+        bits[k] = 0;
+        plan[k] = 0;
+        nprv[k] = 0xFFFFFFFFu;
+        sdec[k] = 0xFFFFFFFFu;
+        delay[k] = 0;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < PPL; ++k) {
+      const uint32_t r = k * G + lane < m.NP ? rw[k] : 0u;
+      sem(k) = r;
+      if constexpr (PART) lsem0[k * G + lane] = r;
+    }
+#pragma unroll
+    for (int k = 0; k < SPL; ++k) {
+      const uint32_t n = k * G + lane < m.S ? nw[k] : 0u;
+      lcnt[k * G + lane] = n;
+      if constexpr (PART) lsem0[G * PPL + k * G + lane] = n;
+    }
+#else
 #pragma unroll
     for (int k = 0; k < TPL; ++k) {
       const int hk = lane + G * k;
@@ -768,15 +832,16 @@ struct WEnv {
       const int p = k * G + lane;
       const uint32_t r = p < m.NP ? ld(sem_words(), pix(p)) : 0u;
       sem(k) = r;
-      if constexpr (PART) sem0[k] = r;
+      if constexpr (PART) lsem0[k * G + lane] = r;
     }
 #pragma unroll
     for (int k = 0; k < SPL; ++k) {
       const int sw = k * G + lane;
       const uint32_t n = sw < m.S ? ld(s.counts, cix(sw)) : 0u;
       lcnt[k * G + lane] = n;
-      if constexpr (PART) cnt0[k] = n;
+      if constexpr (PART) lsem0[G * PPL + k * G + lane] = n;
     }
+#endif
     now = U(ld(s.elapsed, e));
     flags = U(ld(s.eflags, e));
     epoch = U(ld(s.epoch, e));
@@ -817,15 +882,27 @@ struct WEnv {
       }
     }
     // (PART: a round changes a handful of records and one counter; only those are written back)
+    // (the LDS reads first, then the stores: one wait instead of one per record)
+    uint32_t rw[PPL], r0[PART ? PPL : 1], nw[SPL], n0[PART ? SPL : 1];
+#pragma unroll
+    for (int k = 0; k < PPL; ++k) {
+      rw[k] = sem(k);
+      if constexpr (PART) r0[k] = lsem0[k * G + lane];
+    }
+#pragma unroll
+    for (int k = 0; k < SPL; ++k) {
+      nw[k] = lcnt[k * G + lane];
+      if constexpr (PART) n0[k] = lsem0[G * PPL + k * G + lane];
+    }
 #pragma unroll
     for (int k = 0; k < PPL; ++k) {
       const int p = k * G + lane;
-      if (p < m.NP && (!PART || sem(k) != sem0[k])) st(sem_words(), pix(p), sem(k));
+      if (p < m.NP && (!PART || rw[k] != r0[PART ? k : 0])) st(sem_words(), pix(p), rw[k]);
     }
 #pragma unroll
     for (int k = 0; k < SPL; ++k) {
       const int sw = k * G + lane;
-      if (sw < m.S && (!PART || lcnt[k * G + lane] != cnt0[k])) st(s.counts, cix(sw), lcnt[k * G + lane]);
+      if (sw < m.S && (!PART || nw[k] != n0[PART ? k : 0])) st(s.counts, cix(sw), nw[k]);
     }
     uint32_t err = 0;
 #pragma unroll
@@ -2136,13 +2213,15 @@ template <int PPL, int SPL, int TW, bool TRACE, bool PART = false, bool TIMED = 
 __device__ void run(const SflMap& m, const SflState& s, const SflCtl& c, const SflPart* P = nullptr) {
   using V = WEnv<PPL, SPL, TW, PART>;
   // semaphores, counters, prefetch records, rng, timetable (PART: one record, timetable from the map)
-  constexpr int LDS_WORDS = 64 * (PPL + SPL) + V::PF_SLOTS * PF_WORDS + 12 + (PART ? 0 : TW * 8);
+  // (PART: the launch's initial records / counters in place of the timetable copy)
+  constexpr int LDS_WORDS = 64 * (PPL + SPL) + V::PF_SLOTS * PF_WORDS + 12 + (PART ? 64 * (PPL + SPL) : TW * 8);
   const int lane = (int)__lane_id();
   const uint32_t e = uni((uint32_t)((blockIdx.x * blockDim.x + threadIdx.x) >> 6));
   if (e >= s.E) return;
   constexpr int WPB = TW > 64 ? 1 : SFL_WAVE_BLOCK / 64;  // waves (envs) per block (sfl.hip launches)
   __shared__ uint32_t lds[WPB * LDS_WORDS];
   V v(m, s, e, lane, lds + (threadIdx.x >> 6) * LDS_WORDS, P);
+  if constexpr (PART) v.lsem0 = lds + (threadIdx.x >> 6) * LDS_WORDS + 64 * (PPL + SPL) + V::PF_SLOTS * PF_WORDS + 12;
   PhaseTimer tm;
   if constexpr (TIMED) tm.start(c.phase_cyc != nullptr && blockIdx.x % TM_SAMPLE == 0u);
   v.load();
