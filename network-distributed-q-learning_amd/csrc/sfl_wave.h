@@ -361,10 +361,13 @@ struct WEnv {
   int32_t req_dst_v = -1;  // destination of the request (-1: none)
   uint32_t n_upd = 0;      // update records staged
   uint32_t stg = 0;        // next update stage of this launch (the posts' records in program order)
-  // PART: the launch's loaded semaphore records and counters, [64 * (PPL + SPL)] words of the env's LDS region
+  // PART: the launch's loaded semaphore records, [64 * PPL] words of the env's LDS region
   // (store() writes back only what changed).  Held in registers they were spilled, and every conditional
   // store of the write-back then waited for its predecessors (a scratch reload's vmcnt counts stores too)
   uint32_t* lsem0 = nullptr;
+  // PART: switches whose counter changed in this launch, a bitmap of (G * SPL) / 32 words after lsem0 (cset sets
+  // the bit; store() writes back only those counters)
+  uint32_t* ldirty = nullptr;
   // product phase timers (the TIMED kernels that learn() / test() run; sfl_get_phase_cycles): decide<true>
   // stamps the end of its observe and epsilon-greedy sections on a sampled wavefront (tm_on); run_groups
   // reads the stamps from a deciding lane after the (divergent) decide block
@@ -501,6 +504,9 @@ struct WEnv {
   __device__ __forceinline__ uint32_t cget(int sw) const { return U(lcnt[sw]); }
   __device__ __forceinline__ void cset(int sw, uint32_t v) {
     lcnt[sw] = v;  // wave-uniform value from every lane
+    if constexpr (PART) {
+      if (lid() == 0) atomicOr(&ldirty[sw >> 5], 1u << (sw & 31));
+    }
   }
   __device__ __forceinline__ uint32_t cget_var(int sw) const { return lcnt[sw]; }  // per-lane index
   // train h's value of a per-train register (h wave-uniform)
@@ -801,7 +807,7 @@ struct WEnv {
     for (int k = 0; k < SPL; ++k) {
       const uint32_t n = k * G + lane < m.S ? nw[k] : 0u;
       lcnt[k * G + lane] = n;
-      if constexpr (PART) lsem0[G * PPL + k * G + lane] = n;
+
     }
 #else
 #pragma unroll
@@ -839,9 +845,12 @@ struct WEnv {
       const int sw = k * G + lane;
       const uint32_t n = sw < m.S ? ld(s.counts, cix(sw)) : 0u;
       lcnt[k * G + lane] = n;
-      if constexpr (PART) lsem0[G * PPL + k * G + lane] = n;
+
     }
 #endif
+    if constexpr (PART) {
+      if (lane < 2 * SPL) ldirty[lane] = 0u;
+    }
     now = U(ld(s.elapsed, e));
     flags = U(ld(s.eflags, e));
     epoch = U(ld(s.epoch, e));
@@ -892,7 +901,7 @@ struct WEnv {
 #pragma unroll
     for (int k = 0; k < SPL; ++k) {
       nw[k] = lcnt[k * G + lane];
-      if constexpr (PART) n0[k] = lsem0[G * PPL + k * G + lane];
+      if constexpr (PART) n0[k] = (ldirty[(k * G + lane) >> 5] >> ((k * G + lane) & 31)) & 1u;
     }
 #pragma unroll
     for (int k = 0; k < PPL; ++k) {
@@ -902,7 +911,7 @@ struct WEnv {
 #pragma unroll
     for (int k = 0; k < SPL; ++k) {
       const int sw = k * G + lane;
-      if (sw < m.S && (!PART || nw[k] != n0[PART ? k : 0])) st(s.counts, cix(sw), nw[k]);
+      if (sw < m.S && (!PART || n0[PART ? k : 0] != 0u)) st(s.counts, cix(sw), nw[k]);
     }
     uint32_t err = 0;
 #pragma unroll
@@ -2214,14 +2223,17 @@ __device__ void run(const SflMap& m, const SflState& s, const SflCtl& c, const S
   using V = WEnv<PPL, SPL, TW, PART>;
   // semaphores, counters, prefetch records, rng, timetable (PART: one record, timetable from the map)
   // (PART: the launch's initial records / counters in place of the timetable copy)
-  constexpr int LDS_WORDS = 64 * (PPL + SPL) + V::PF_SLOTS * PF_WORDS + 12 + (PART ? 64 * (PPL + SPL) : TW * 8);
+  constexpr int LDS_WORDS = 64 * (PPL + SPL) + V::PF_SLOTS * PF_WORDS + 12 + (PART ? 64 * PPL + 2 * SPL : TW * 8);
   const int lane = (int)__lane_id();
   const uint32_t e = uni((uint32_t)((blockIdx.x * blockDim.x + threadIdx.x) >> 6));
   if (e >= s.E) return;
   constexpr int WPB = TW > 64 ? 1 : SFL_WAVE_BLOCK / 64;  // waves (envs) per block (sfl.hip launches)
   __shared__ uint32_t lds[WPB * LDS_WORDS];
   V v(m, s, e, lane, lds + (threadIdx.x >> 6) * LDS_WORDS, P);
-  if constexpr (PART) v.lsem0 = lds + (threadIdx.x >> 6) * LDS_WORDS + 64 * (PPL + SPL) + V::PF_SLOTS * PF_WORDS + 12;
+  if constexpr (PART) {
+    v.lsem0 = lds + (threadIdx.x >> 6) * LDS_WORDS + 64 * (PPL + SPL) + V::PF_SLOTS * PF_WORDS + 12;
+    v.ldirty = v.lsem0 + 64 * PPL;
+  }
   PhaseTimer tm;
   if constexpr (TIMED) tm.start(c.phase_cyc != nullptr && blockIdx.x % TM_SAMPLE == 0u);
   v.load();
