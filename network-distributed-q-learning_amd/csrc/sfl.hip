@@ -222,6 +222,66 @@ __global__ void __launch_bounds__(256) k_part_compact(const sfl::SflPart* __rest
   }
   if (ovf) s->err[e] |= ovf;
 }
+// part_answer_one (sfl_part.h) with its table reads issued together: the switch's action sources and compact
+// columns (8 bytes each), the block's width and offsets, then the row's columns, then the same comparisons in
+// the same order (row_max, max_action: bit-identical results).  Round 3: the generic version walks row_val
+// per action, a chain of dependent L2 reads per request (12.6 us of a 178-us round).
+__device__ __forceinline__ void part_answer_fast(const sfl::SflMap& m, const sfl::SflPart& P, const sfl::PartReq& r,
+                                                 sfl::PartRep& out) {
+  const int port = r.port, sw = port >> 2, slot = port & 3;
+  const int na = m.sw_na[sw];
+  const uint2 srcw = *(const uint2*)(m.act_src + (size_t)sw * 8);
+  const uint2 jw = *(const uint2*)(m.act_j + (size_t)sw * 8);
+  const int w = m.q_w[port];
+  const double* row = P.q_own + (size_t)r.genv * P.q_own_per_env + P.q_off_own[port] + (size_t)r.state * (uint32_t)w;
+  double rv[8];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) rv[c] = row[c < w ? c : 0];
+  auto col = [&](int c) -> double {
+    double v = rv[0];
+#pragma unroll
+    for (int k = 1; k < 8; ++k) v = c == k ? rv[k] : v;
+    return v;
+  };
+  auto val = [&](int a) -> double {  // row_val
+    if (a == na - 1) return col(w - 1);
+    const uint32_t src = ((a < 4 ? srcw.x : srcw.y) >> (8 * (a & 3))) & 0xFFu;
+    if (src == (uint32_t)slot) return col((int)(((a < 4 ? jw.x : jw.y) >> (8 * (a & 3))) & 0xFFu));
+    return m.default_q;
+  };
+  double mx = val(0);
+  int best = 0;
+  for (int a = 1; a < na; ++a) {
+    const double v = val(a);
+    if (v > mx) {
+      mx = v;
+      best = a;
+    }
+  }
+  out.mq = mx;  // (row_max: the same maximum over the same sequence)
+  out.pad = 0;
+  if (r.flags & 1u) {
+    out.action = -1;
+    return;
+  }
+  const uint32_t rid = P.row_own[port] + r.state;
+  atomicOr(&P.touched_own[(size_t)r.genv * P.own_words + (rid >> 5)], 1u << (rid & 31u));
+  if ((r.amask >> best) & 1u) {
+    out.action = best;
+    return;
+  }
+  int arg = -1;
+  double amx = 0.0;
+  for (int a = 0; a < na; ++a) {
+    if (!((r.amask >> a) & 1u)) continue;
+    const double v = val(a);
+    if (arg < 0 || v > amx) {
+      arg = a;
+      amx = v;
+    }
+  }
+  out.action = arg;
+}
 __global__ void k_part_answer(const sfl::SflMap* __restrict__ m, const sfl::SflPart* __restrict__ P,
                               const sfl::PartReq* __restrict__ in, sfl::PartRep* __restrict__ out) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -229,7 +289,11 @@ __global__ void k_part_answer(const sfl::SflMap* __restrict__ m, const sfl::SflP
   const size_t g = i / cap, k = i % cap + 1;
   if (g >= (size_t)P->world) return;
   const size_t base = g * (cap + 1);
-  if (k <= in[base].genv) sfl::part_answer_one(*m, *P, in[base + k], out[base + k]);
+#ifdef SFL_ANSWER_GENERIC
+  if (k <= in[base].genv) sfl::part_answer_one(*m, *P, in[base + k], out[base + k]);  // (tuning A/B)
+#else
+  if (k <= in[base].genv) part_answer_fast(*m, *P, in[base + k], out[base + k]);
+#endif
 }
 // stage 0 (the pending updates and key-set inserts: one per env and cell) in parallel over a bounded grid
 // (a grid-stride loop to each segment's header count: the segments are sized for the worst case, 16 records
