@@ -110,7 +110,12 @@ constexpr int kNumVariants = 10;
 // registers and every semaphore record fits the 32-bit LDS word (sfl_wave.h r_pack: start tick
 // -8192..8191, span <= 511).  SFL_KERNEL=scalar forces k_run.  why: when non-null, the reason a
 // map is not eligible (the caller reports it; the lane-per-env body is 15-45x slower).
-inline int choose_variant(const sfl_map_desc* md, bool backend_has_wave, std::string* why = nullptr) {
+// A batch too small to fill the device at the default group size (fewer than kFillWaves wavefronts: 4 per SIMD
+// of MI355X's 1,024) takes two envs per wavefront instead of four: c2 at its stated 4,096 envs 316 M vs 276 M
+// agent-env-steps/s (G = 64: 313 M), while c3 at 16,384 envs -- 4,096 wavefronts at G = 16 -- keeps G = 16
+// (1,275 M vs 982 M at G = 64; profiles/r03d_group_size_*.json).
+constexpr uint64_t kFillWaves = 4096;
+inline int choose_variant(const sfl_map_desc* md, bool backend_has_wave, std::string* why = nullptr, uint64_t n_envs = 0) {
   if (!backend_has_wave) return 0;
   const char* env = getenv("SFL_KERNEL");
   if (env && strcmp(env, "scalar") == 0) return 0;
@@ -135,7 +140,8 @@ inline int choose_variant(const sfl_map_desc* md, bool backend_has_wave, std::st
   if (md->q_per_env >= (1ull << 32)) return no("Q-table beyond 2^32 cells per env");
   if ((int64_t)md->H * md->W >= (1 << 20) - 1) return no("grid beyond 2^20 cells");
   const char* gs = getenv("SFL_WAVE_G");
-  const int want_g = gs ? atoi(gs) : SFL_DEFAULT_G;
+  int want_g = gs ? atoi(gs) : SFL_DEFAULT_G;
+  if (!gs && n_envs > 0 && want_g < 32 && n_envs * (uint64_t)want_g / 64 < kFillWaves) want_g = 32;
   auto fits = [&](int v) {
     const WaveShape& w = kVariants[v];
     return md->S * 4 <= w.G * w.PPL && md->S <= w.G * w.SPL && md->T <= w.TW;
@@ -175,7 +181,7 @@ int create(const sfl_map_desc* md, const sfl_hparams* hp, uint32_t n_envs, const
   h->h_q_w.assign(md->q_w, md->q_w + (size_t)md->S * 4);
   h->h_q_off.assign(md->q_off, md->q_off + (size_t)md->S * 4);
   h->h_row_base.assign(md->row_base, md->row_base + (size_t)md->S * 4);
-  h->variant = choose_variant(md, B::kHasWave, &h->variant_note);
+  h->variant = choose_variant(md, B::kHasWave, &h->variant_note, n_envs);
   SflMap& m = h->map;
   const size_t HW = (size_t)md->H * md->W, NP = (size_t)md->S * 4, S = md->S, T = md->T;
   m.H = md->H;
