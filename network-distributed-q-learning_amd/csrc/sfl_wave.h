@@ -49,6 +49,9 @@ namespace wave {
 #ifndef SFL_LOAD_BATCH
 #define SFL_LOAD_BATCH 1  // WEnv::load issues every state load before using any (0: per-record conditional loads)
 #endif
+#ifndef SFL_TICK_HOIST
+#define SFL_TICK_HOIST 1  // tick: the train slots' move-table loads issued together (+0.6 %, profiles/r03_ab_regalloc.txt)
+#endif
 #ifndef SFL_TICK_REMMIN
 #define SFL_TICK_REMMIN 5  // ... and one of them has fewer than this many decisions left (0: hold regardless)
 #endif
@@ -1007,6 +1010,18 @@ struct WEnv {
       tt1[k] = *(const vec_t<int32_t, 4>*)(ltt + 8 * (mine_(k) ? lid() + G * k : 0) + 4);
     }
     // pass 1: plan pop + prediction, malfunction draw, action preprocessing, desired move
+#if SFL_TICK_HOIST
+    // (the slots' move-table rows loaded together, clamped: inside each slot's exec-masked block the
+    // second load waited for the first slot's work)
+    u4 mrows[TPL];
+#pragma unroll
+    for (int k = 0; k < TPL; ++k) {
+      const bool ok = mine_(k);
+      const int pc = pos[k] >= 0 ? pos[k] : tt1[k][0];
+      const int pd = pos[k] >= 0 ? (int)tb_dir(bits[k]) : (int)((uint32_t)tt1[k][3] & 0xFFu);
+      mrows[k] = ld((const u4*)m.move_tab, (size_t)((uint32_t)(ok ? pc : 0) * 4u + (uint32_t)(ok ? pd : 0)));
+    }
+#endif
     bool mover[TPL];
     int32_t desired[TPL], pred[TPL];
     uint32_t aux[TPL];
@@ -1028,7 +1043,11 @@ struct WEnv {
         // every check_action of this pass is at (pc, pd): one 16-byte load of the move-table row
         const int pc = p0 >= 0 ? p0 : t_init_cell;
         const int pd = p0 >= 0 ? (int)dir : (int)t_init_dir;
+#if SFL_TICK_HOIST
+        const u4 mrow = mrows[k];
+#else
         const u4 mrow = ld((const u4*)m.move_tab, (size_t)((uint32_t)pc * 4u + (uint32_t)pd));
+#endif
         auto mv_of = [&](uint32_t a) -> Move {
           const uint32_t q = a & 3u;
           return unpack_move(q == 0 ? mrow[0] : q == 1 ? mrow[1] : q == 2 ? mrow[2] : mrow[3]);
@@ -1274,14 +1293,27 @@ struct WEnv {
     mf_mask = MF;
     SFL_LAP(14);
     // _check_active_switch (switch_env.py:427-485)
+#if SFL_TICK_HOIST
+    Move amv[TPL];
+#pragma unroll
+    for (int k = 0; k < TPL; ++k) {
+      const bool ok = mine_(k) && pos[k] >= 0;
+      const uint32_t nxt = pl_len(plan[k]) ? pl_front(plan[k]) : A_FWD;
+      amv[k] = check_action<false>(nxt, ok ? pos[k] : 0, ok ? (int)tb_dir(bits[k]) : 0);
+    }
+#endif
     bool act[TPL];
 #pragma unroll
     for (int k = 0; k < TPL; ++k) {
       act[k] = false;
       const uint32_t st4 = tb_state(bits[k]);
       if (mine_(k) && pos[k] >= 0 && st4 != S_WAITING) {
+#if SFL_TICK_HOIST
+        const Move mv = amv[k];
+#else
         const uint32_t nxt = pl_len(plan[k]) ? pl_front(plan[k]) : A_FWD;
         const Move mv = check_action<false>(nxt, pos[k], (int)tb_dir(bits[k]));
+#endif
         if (mv.cell >= 0) {
           const int sw_at = dest_sw(mv);
           if (sw_at >= 0) {
