@@ -8,14 +8,20 @@ tick in between and episodes restarting as they end).  N GPUs: one process per G
 own 65,536 envs (weak scaling, no collective on the data path; the reference's parallelism is an
 embarrassingly parallel seed sweep, hyperparam_tuning.py:85-91).
 
-Usage: python bench.py [--gpus N --steps K --warmup W]; N > 1 is launched by torch.distributed.run.
+Usage: python bench.py [--gpus N --steps K --warmup W].  N > 1 runs one rank per GPU: under
+torch.distributed.run (the driver's launch) every rank checks WORLD_SIZE == N and that N devices are
+visible; started without it, bench.py launches ``torch.distributed.run --nproc-per-node N`` itself as a
+child process (before any HIP call) and exits with its return code.
 """
 from __future__ import annotations
 
 import argparse
+import glob
 import importlib
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -109,14 +115,83 @@ def cpu_oracle_baseline(sc, seconds: float):
                        f"(from episode start, incl. the Q-table init)")
 
 
-def dist_setup(par, local: int):
+def visible_gpus() -> int:
+    """GPUs this process may use, counted without any HIP call: the KFD topology's GPU nodes (gpu_id != 0),
+    restricted by ROCR_VISIBLE_DEVICES / HIP_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES when set."""
+    n = 0
+    for f in glob.glob("/sys/class/kfd/kfd/topology/nodes/*/gpu_id"):
+        try:
+            n += int(open(f).read().strip() or "0") != 0
+        except (OSError, ValueError):
+            pass
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            n = min(n, len([x for x in v.split(",") if x.strip() != ""]))
+    return n
+
+
+def rehearsal() -> bool:
+    """SFL_DIST_BACKEND=gloo: the multi-rank path rehearsed with several ranks sharing one device (or the host
+    build): the launcher, sharding and reductions, not the RCCL transport."""
+    return os.environ.get("SFL_DIST_BACKEND", "nccl") != "nccl"
+
+
+def launch_or_check(args, argv) -> int | None:
+    """The contract's --gpus N (the reference's scale-out is N independent processes,
+    hyperparam_tuning.py:85-91).  Outside torch.distributed.run with N > 1: launch N ranks as a child
+    ``torch.distributed.run`` (never exec: this process has not touched the GPU, and the child is a new
+    process) and return its exit code.  Inside it: return 2 unless WORLD_SIZE == N and, for RCCL, N devices
+    are visible.  None: go on in this process."""
+    ws = os.environ.get("WORLD_SIZE")
+    if ws is None:
+        if args.gpus <= 1:
+            return None
+        if not rehearsal() and not args.rehearse_on_host and visible_gpus() < args.gpus:
+            print(f"bench.py: --gpus {args.gpus} needs {args.gpus} visible GPUs, found {visible_gpus()}; refusing to "
+                  f"time fewer (SFL_DIST_BACKEND=gloo rehearses several ranks on one device)", file=sys.stderr)
+            return 2
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+        s.close()
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+               "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+        print("bench.py: launching " + " ".join(cmd[1:]), file=sys.stderr, flush=True)
+        return subprocess.run(cmd).returncode
+    if int(ws) != args.gpus:
+        print(f"bench.py: WORLD_SIZE={ws} but --gpus {args.gpus}: the job would report a different GPU count than "
+              f"it runs on; refusing", file=sys.stderr)
+        return 2
+    if not rehearsal() and not args.rehearse_on_host:
+        local_ws = int(os.environ.get("LOCAL_WORLD_SIZE", ws))
+        if visible_gpus() < local_ws:
+            print(f"bench.py: {local_ws} ranks on this node need {local_ws} visible GPUs, found {visible_gpus()}; "
+                  f"refusing", file=sys.stderr)
+            return 2
+    return None
+
+
+def dist_setup(par, local: int, host: bool = False):
     """torch.distributed for the bench: RCCL ("nccl") over the GPUs of the node, one per rank.
     SFL_DIST_BACKEND=gloo and SFL_DEVICE=<index> rehearse the multi-rank path with several ranks
-    on one GPU (the launcher, sharding and reductions; not the RCCL transport)."""
-    backend = os.environ.get("SFL_DIST_BACKEND", "nccl")
+    on one GPU (the launcher, sharding and reductions; not the RCCL transport).  ``host``: the
+    --rehearse-on-host run (gloo, no device)."""
+    backend = "gloo" if host else os.environ.get("SFL_DIST_BACKEND", "nccl")
     dev = int(os.environ.get("SFL_DEVICE", local))
-    dist = par.init(backend) if backend != "nccl" else par.init("nccl")
+    dist = par.init(backend)
     return dist, dev, ("cuda" if backend == "nccl" else "cpu")
+
+
+def rank_devices(dist, dev: int, device=None):
+    """The device index of every rank, in rank order."""
+    if dist is None:
+        return [dev]
+    import torch
+    t = torch.tensor([dev], dtype=torch.int64, device=device)
+    parts = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(parts, t)
+    return [int(p.item()) for p in parts]
 
 
 def pmc_profile(lib, workload: str):
@@ -210,30 +285,45 @@ def main():
     ap.add_argument("--partition", action="store_true",
                     help="graph-partitioned mode (BASELINE configs[4]): switch agents owned by ranks, RCCL all-to-all "
                          "of row lookups and updates; defaults to --config c5 --envs 16384 (238 GB of owned Q rows per GPU)")
+    ap.add_argument("--rehearse-on-host", action="store_true",
+                    help="TEST ONLY: run the ranks on the host build of the kernel body (libsfl_hostsim.so, gloo) to "
+                         "rehearse the launcher without a GPU; the line says so and is no measurement")
     args = ap.parse_args()
+    rc = launch_or_check(args, sys.argv[1:])
+    if rc is not None:
+        sys.exit(rc)
     if args.experimental:
         os.environ["SFL_EXPERIMENTAL"] = "1"
     if args.partition:
         return bench_partition(args)
 
     import torch
+    host = args.rehearse_on_host
     par = importlib.import_module(PKG + ".parallel")
     world, rank, local = par.world()
-    dist, dev, red_dev = dist_setup(par, local)
-    torch.cuda.set_device(dev)
+    dist, dev, red_dev = dist_setup(par, local, host)
+    if not host:
+        torch.cuda.set_device(dev)
+    devices = rank_devices(dist, -1 if host else dev, device=red_dev)
 
     mapgen = importlib.import_module(PKG + ".mapgen")
     comp = importlib.import_module(PKG + ".compiler")
     runtime = importlib.import_module(PKG + ".runtime")
+    build = importlib.import_module(PKG + ".build")
     if rank == 0:  # (re)build if the library is not from these sources; the other ranks wait for it
-        importlib.import_module(PKG + ".build").build_hip()
+        build.build_hostsim() if host else build.build_hip()
     if dist is not None:
         dist.barrier()
     sc = mapgen.make_config(args.config)
     cm = comp.compile_scenario(sc)
     E = args.envs
     seeds = par.shard_seeds(450565, E, rank)
-    b = runtime.Batch(cm, HP, seeds, device=dev)
+    lib = None
+    if host:
+        _lib = importlib.import_module(PKG + "._lib")
+        lib = _lib.Lib(build.build_hostsim())
+        lib.check_fresh()
+    b = runtime.Batch(cm, HP, seeds, device=dev, lib=lib)
     b.learn_begin()
     b.apply_qinit()
     for _ in range(args.warmup):
@@ -242,7 +332,8 @@ def main():
     def barrier():
         if dist is not None:
             dist.barrier()
-        torch.cuda.synchronize()
+        if not host:
+            torch.cuda.synchronize()
 
     barrier()
     t0 = time.perf_counter()
@@ -303,9 +394,14 @@ def main():
             "library": library_info(b.lib),
             "world_size": world,
             "backend": (dist.get_backend() if dist is not None else None),
+            "devices": devices,
             **pfield,
         }
-        if world == 1 and not args.no_cpu:
+        if host:
+            res["rehearsal"] = ("--rehearse-on-host: every rank ran the host build of the kernel body; a launcher "
+                                "rehearsal, not a GPU measurement")
+            res["roofline"] = None
+        if world == 1 and not args.no_cpu and not host:
             res["cpu_baseline"] = cpu_baseline(cm, args.cpu_seconds, args.config)
             res["cpu_oracle_baseline"] = cpu_oracle_baseline(sc, args.cpu_seconds / 2)
         print(json.dumps(res), flush=True)
@@ -322,8 +418,11 @@ def bench_partition(args):
     par = importlib.import_module(PKG + ".parallel")
     part = importlib.import_module(PKG + ".partition")
     world, rank, local = par.world()
+    if args.rehearse_on_host:
+        raise SystemExit("bench.py: --rehearse-on-host covers the env-sharded bench, not --partition")
     dist, dev, red_dev = dist_setup(par, local)
     torch.cuda.set_device(dev)
+    devices = rank_devices(dist, dev, device=red_dev)
     mapgen = importlib.import_module(PKG + ".mapgen")
     comp = importlib.import_module(PKG + ".compiler")
     cfg = args.config if args.config != "c3" else "c5"
@@ -400,6 +499,7 @@ def bench_partition(args):
             "library": library_info(pb.lib),
             "world_size": world,
             "backend": (dist.get_backend() if dist is not None else None),
+            "devices": devices,
             **pfield,
         }
         print(json.dumps(res), flush=True)

@@ -1,0 +1,67 @@
+"""bench.py --gpus N runs N ranks or refuses (the driver's SCALE runs time exactly what they report).
+
+* Without torch.distributed.run, ``bench.py --gpus 2`` launches ``torch.distributed.run --nproc-per-node 2``
+  as a child process; here the ranks run the host build of the kernel body over gloo
+  (``--rehearse-on-host``), end to end: sharding, timing max / decision sum, parity reduction, rank-0 line.
+* Under a launcher whose WORLD_SIZE differs from --gpus, every rank refuses.
+* With fewer visible GPUs than --gpus (none here), the launcher refuses before starting anything.
+"""
+import json
+import os
+import subprocess
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _env(**kw):
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT",
+                        "SFL_DIST_BACKEND", "SFL_DEVICE")}
+    env.update(kw)
+    return env
+
+
+def _bench(args, env, timeout=300):
+    return subprocess.run([sys.executable, os.path.join(REPO, "bench.py")] + args, cwd=REPO, env=env,
+                          capture_output=True, text=True, timeout=timeout)
+
+
+def test_gpus_2_launches_two_ranks_end_to_end():
+    r = _bench(["--gpus", "2", "--rehearse-on-host", "--config", "c2", "--envs", "4", "--decisions", "32",
+                "--steps", "2", "--warmup", "1", "--verify-envs", "2"], _env(OMP_NUM_THREADS="2"))
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "launching" in r.stderr and "--nproc-per-node=2" in r.stderr
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout  # rank 0 only
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == 2 and res["world_size"] == 2 and res["backend"] == "gloo"
+    assert res["devices"] == [-1, -1]
+    assert res["config"]["parallelism"] == "env-batch dp2"
+    assert res["parity"] == "ok" and res["parity_envs_checked"] == 4, res
+    assert "rehearsal" in res and res["roofline"] is None
+    # every rank's decisions are in the job's total: 2 ranks x 4 envs x 32 decisions x 2 timed steps
+    assert abs(res["value"] * res["ms_per_step"] * 1e-3 * res["steps"] - 2 * 4 * 32 * 2) < 1e-6 * res["value"] + 1
+
+
+def test_world_size_other_than_gpus_is_refused():
+    r = _bench(["--gpus", "3", "--steps", "1"], _env(WORLD_SIZE="2", RANK="0", LOCAL_RANK="0"), timeout=60)
+    assert r.returncode == 2
+    assert "WORLD_SIZE=2 but --gpus 3" in r.stderr
+    assert not r.stdout.strip()
+
+
+def test_too_few_gpus_is_refused_before_launch():
+    r = _bench(["--gpus", "2", "--steps", "1"], _env(HIP_VISIBLE_DEVICES=""), timeout=60)
+    assert r.returncode == 2
+    assert "needs 2 visible GPUs, found 0" in r.stderr
+    assert "launching" not in r.stderr and not r.stdout.strip()
+
+
+def test_ranks_refuse_without_devices():
+    # under torch.distributed.run with RCCL: a node with fewer GPUs than ranks refuses on every rank
+    r = _bench(["--gpus", "2", "--steps", "1"],
+               _env(WORLD_SIZE="2", LOCAL_WORLD_SIZE="2", RANK="0", LOCAL_RANK="0", HIP_VISIBLE_DEVICES=""),
+               timeout=60)
+    assert r.returncode == 2
+    assert "2 ranks on this node need 2 visible GPUs, found 0" in r.stderr
