@@ -211,6 +211,7 @@ def pmc_profile(lib, workload: str):
 
 def library_info(lib):
     return {"file": os.path.relpath(lib.path, REPO), "build_id": lib.build_id, "defines": lib.defines,
+            "flags": lib.flags,
             "experimental": bool(lib.experimental)}
 
 

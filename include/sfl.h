@@ -220,7 +220,11 @@ int sfl_part_get_q(sfl_handle* h, uint32_t global_env, double* q, uint32_t* touc
  * observation it emits (agent_iter pops it, last() / observe() read it: switch_env.py:616-630, 668-675,
  * observer.py:246-308) -- or reports the episode's end (agent = -1; the next call resets:
  * switch_env.py:93-158).  actions == null (or an action < 0) applies nothing and re-emits the pending
- * observation.  Output arrays are host pointers, [n_envs] unless stated; null skips one. */
+ * observation; SFL_ACTION_RESET resets the env where it stands (env.reset() in the middle of an episode:
+ * the same reset as at an episode end, switch_env.py:93-158) and emits the new episode's first observation.
+ * An action outside the deciding switch's action space is refused (E_BAD_ACTION, switch_env.py:213-215)
+ * without touching the env.  Output arrays are host pointers, [n_envs] unless stated; null skips one. */
+#define SFL_ACTION_RESET (-2)
 typedef struct {
   const int32_t* actions;  /* in: action for each env's pending observation (< 0 or null: none) */
   int32_t* agent;          /* deciding switch index of the emitted observation; -1: the episode ended */

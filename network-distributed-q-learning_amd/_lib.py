@@ -126,6 +126,7 @@ class Lib:
             raise SflError("ABI version mismatch")
         self.build_id = self.dll.sfl_build_id().decode()
         self.defines = ""
+        self.flags = ""
         self.experimental = False
 
     def check_fresh(self, allow_experimental: bool = False):
@@ -136,18 +137,21 @@ class Lib:
         from . import build
         want = build.product_build_id()
         self.defines = build.built_defines(self.path) or ""
-        if self.build_id == want and not self.defines:
+        self.flags = build.built_flags(self.path) or ""
+        tuned = bool(self.defines or self.flags)
+        if self.build_id == want and not tuned:
             self.experimental = False
             return
-        if allow_experimental and self.defines and self.build_id == build.build_id(self.defines.split()):
+        if allow_experimental and tuned and self.build_id == build.build_id(self.defines.split(), self.flags.split()):
             self.experimental = True
             return
-        if self.defines and allow_experimental:
-            raise SflError(f"{self.path} is stale: a tuning / experiment build (defines: {self.defines}) of other "
-                           f"sources than the tree's (rebuild it)")
-        if self.defines:
-            raise SflError(f"{self.path} is a tuning / experiment build (defines: {self.defines}), not the product "
-                           f"library; set SFL_EXPERIMENTAL=1 (bench.py --experimental) to run it anyway")
+        what = f"defines: {self.defines or '-'}, flags: {self.flags or '-'}"
+        if tuned and allow_experimental:
+            raise SflError(f"{self.path} is stale: a tuning / experiment build ({what}) of other sources than the "
+                           f"tree's (rebuild it)")
+        if tuned:
+            raise SflError(f"{self.path} is a tuning / experiment build ({what}), not the product library; set "
+                           f"SFL_EXPERIMENTAL=1 (bench.py --experimental) to run it anyway")
         raise SflError(f"{self.path} is stale: built as {self.build_id[:12]}, the tree's product build is {want[:12]} "
                        f"(rebuild: python -c 'import __graft_entry__ as g; g.build()')")
 

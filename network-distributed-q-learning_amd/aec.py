@@ -21,6 +21,7 @@ from .compiler import CompiledMap
 from .runtime import Batch, _ptr
 
 # the learner's hyper-parameters do not enter the env (no epsilon draw, no Q-table access)
+ACTION_RESET = -2  # include/sfl.h SFL_ACTION_RESET: reset the env where it stands (env.reset() mid-episode)
 _ENV_HP = dict(gamma=1.0, epsilon=0.0, epsilon_decay_rate=1.0, lr=0.0, lr_decay_rate=1.0, default_q=0.0)
 
 
@@ -62,12 +63,24 @@ class AECBatch:
         self.batch.close()
 
     def step(self, actions: Optional[Sequence[int]] = None) -> Dict[str, np.ndarray]:
-        """Apply ``actions[e]`` to each env's pending observation (None / < 0: none) and run every env to its
-        next observation or episode end.  Returns the output arrays (views, valid until the next call)."""
+        """Apply ``actions[e]`` to each env's pending observation (None / < 0: none; ``ACTION_RESET``: reset the env
+        where it stands) and run every env to its next observation or episode end.  Returns the output arrays (views, valid until the next call)."""
         if actions is None:
             self._act[:] = -1
         else:
-            self._act[:] = np.asarray(actions, np.int32)
+            a = np.asarray(actions, np.int64)
+            if a.shape != (self.E,):
+                raise ValueError(f"step: {a.shape} actions for {self.E} envs")
+            # the reference asserts action_space(agent).contains(action) (switch_env.py:213-215)
+            ag = self.out["agent"]
+            pend = (ag >= 0) & (a >= 0)
+            na = np.asarray(self.cm.n_actions, np.int64)[np.where(pend, ag, 0)]
+            bad = np.nonzero(pend & (a >= na))[0]
+            if len(bad):
+                e = int(bad[0])
+                raise ValueError(f"step: action {int(a[e])} of env {e} is outside switch {int(ag[e])}'s action space "
+                                 f"Discrete({int(na[e])})")
+            self._act[:] = np.where(a == ACTION_RESET, ACTION_RESET, np.where(a < 0, -1, a)).astype(np.int32)
         self._io.actions = _ptr(self._act, C.c_int32)
         self.lib.check(self.lib.dll.sfl_env_step(self.batch.h, C.byref(self._io)), "sfl_env_step")
         return self.out

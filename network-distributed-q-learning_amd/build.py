@@ -26,6 +26,7 @@ SOURCES = ["sfl.hip", "sfl_core.h", "sfl_wave.h", "sfl_rng.h", "sfl_engine.h", "
            "sfl_experiment.h", os.path.join("..", "..", "include", "sfl.h")]
 _MARK = re.compile(rb"SFL_BUILD_ID:([0-9a-f]{40})")
 _DEFS = re.compile(rb"SFL_BUILD_DEFS:\[([^\]\x00]*)\]")
+_FLAGS = re.compile(rb"SFL_BUILD_FLAGS:\[([^\]\x00]*)\]")
 PRODUCT_LIB = os.path.join(HERE, "libsfl.so")
 # timing-only switches whose builds compute wrong results (csrc/sfl_experiment.h)
 EXPERIMENT_PREFIXES = ("SFL_X_", "SFL_AB_")
@@ -62,6 +63,14 @@ def built_defines(path: str):
     return m.group(1).decode() if m else None
 
 
+def built_flags(path: str):
+    """The extra compiler flags recorded in a library file ("" for none; None if it carries no record)."""
+    if not os.path.exists(path):
+        return None
+    m = _FLAGS.search(open(path, "rb").read())
+    return m.group(1).decode() if m else None
+
+
 def built_id(path: str):
     """The build id compiled into a library file (None: missing, or built without one)."""
     if not os.path.exists(path):
@@ -89,7 +98,7 @@ def build_hip(force: bool = False, verbose: bool = False, out: str = None, defin
         defs = " ".join(sorted(defines))
         cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off",
                "-Wno-unused-result", "-Wno-unused-value", f'-DSFL_BUILD_ID="{build_id(defines, flags)}"',
-               f'-DSFL_BUILD_DEFS="{defs}"'] + \
+               f'-DSFL_BUILD_DEFS="{defs}"', f'-DSFL_BUILD_FLAGS="{" ".join(flags)}"'] + \
               [f"-D{d}" for d in defines] + list(flags) + ["-o", out + ".tmp", os.path.join(CSRC, "sfl.hip")]
         if verbose:
             print(" ".join(cmd), flush=True)
@@ -98,21 +107,22 @@ def build_hip(force: bool = False, verbose: bool = False, out: str = None, defin
     return out
 
 
-def build_hostsim(out_dir: str = None, force: bool = False, defines=()) -> str:
+def build_hostsim(out_dir: str = None, force: bool = False, defines=(), flags=()) -> str:
     """The same kernel body compiled for the host CPU (libsfl_hostsim.so, OpenMP over envs): the
     parity tests' host build and bench.py's C++ CPU baseline -- never the product path.  Built
     in-tree so that it travels to the GPU box with the snapshot.  ``defines``: a tuning build (into
-    another ``out_dir`` only; its build id differs, like build_hip's)."""
+    another ``out_dir`` only; its build id differs, like build_hip's); ``flags`` likewise."""
     out_dir = out_dir or HERE
-    defines = list(defines)
-    if defines and os.path.abspath(out_dir) == os.path.abspath(HERE):
-        raise ValueError("build_hostsim: defines are not built into the in-tree host build")
+    defines, flags = list(defines), list(flags)
+    if (defines or flags) and os.path.abspath(out_dir) == os.path.abspath(HERE):
+        raise ValueError("build_hostsim: defines / flags are not built into the in-tree host build")
     os.makedirs(out_dir, exist_ok=True)
     out = os.path.abspath(os.path.join(out_dir, "libsfl_hostsim.so"))
-    if force or _stale(out, defines):
+    if force or _stale(out, defines, flags):
         cmd = ["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-fopenmp",
-               f'-DSFL_BUILD_ID="{build_id(defines)}"', f'-DSFL_BUILD_DEFS="{" ".join(sorted(defines))}"'] + \
-              [f"-D{d}" for d in defines] + ["-o", out + ".tmp", os.path.join(CSRC, "sfl_hostsim.cpp")]
+               f'-DSFL_BUILD_ID="{build_id(defines, flags)}"', f'-DSFL_BUILD_DEFS="{" ".join(sorted(defines))}"',
+               f'-DSFL_BUILD_FLAGS="{" ".join(flags)}"'] + \
+              [f"-D{d}" for d in defines] + list(flags) + ["-o", out + ".tmp", os.path.join(CSRC, "sfl_hostsim.cpp")]
         subprocess.run(cmd, check=True, cwd=CSRC)
         os.replace(out + ".tmp", out)
     return out

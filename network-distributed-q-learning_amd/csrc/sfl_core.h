@@ -1025,7 +1025,7 @@ SFL_FN void decide_apply(V& v, const Obs& o, int action, Decision& d) {
   bool moving = false;
   uint32_t turn = A_FWD;
   int in_p = pin, out_p = pin;
-  if (action != stop && (pin >> 2) == sw) {
+  if (action != stop && action >= 0 && action < na && (pin >> 2) == sw) {  // (no table read for a bad action)
     const int src = m.act_src[sw * 8 + action];
     if (src == slot) {
       moving = true;
@@ -1367,8 +1367,13 @@ SFL_FN void env_run_ext(const SflMap& m, const SflState& s, const SflCtl& c, uin
   x.agent[e] = -1;
   x.next_sw[e] = -1;
   x.step_now[e] = -1;
-  const int32_t act = x.actions[e];
+  int32_t act = x.actions[e];
   bool applied = false;
+  if (act == -2) {  // SFL_ACTION_RESET (sfl.h), env.reset() mid-episode: the episode-end reset, where the env stands
+    phase = PH_RESET;
+    v.flags &= ~(F_EXT_OBS | F_INFLIGHT);
+    act = -1;
+  }
   while (true) {
     if (phase == PH_RESET) {
       env_reset(v);
@@ -1379,14 +1384,19 @@ SFL_FN void env_run_ext(const SflMap& m, const SflState& s, const SflCtl& c, uin
       if (v.flags & F_TERM) phase = (v.flags & F_INFLIGHT) ? PH_POST : PH_END;
       else if (!queue_empty(v)) phase = (v.flags & F_INFLIGHT) ? PH_POST : PH_DECIDE;
     } else if (phase == PH_DECIDE) {
-      if (!(v.flags & F_EXT_OBS) || applied || act < 0) {
+      const bool apply = (v.flags & F_EXT_OBS) && !applied && act >= 0;
+      uint32_t keep[NW];
+#pragma unroll
+      for (int w = 0; w < NW; ++w) keep[w] = v.msk[0][w];
+      Obs o;
+      decide_observe(v, o, true);
+      // an action outside the switch's action space is refused before it touches the env (the reference's
+      // assert, switch_env.py:213-215): E_BAD_ACTION, and the same observation is emitted again
+      const bool bad = apply && act >= m.sw_na[o.sw];
+      if (bad) v.err |= E_BAD_ACTION;
+      if (!apply || bad) {
         // emit the observation of the queue's first train (agent_iter + last(); the queue is left
         // as it is: the next call observes it again and applies the action)
-        uint32_t keep[NW];
-#pragma unroll
-        for (int w = 0; w < NW; ++w) keep[w] = v.msk[0][w];
-        Obs o;
-        decide_observe(v, o, true);
 #pragma unroll
         for (int w = 0; w < NW; ++w) v.msk[0][w] = keep[w];
         x.agent[e] = o.sw;
@@ -1399,8 +1409,6 @@ SFL_FN void env_run_ext(const SflMap& m, const SflState& s, const SflCtl& c, uin
         v.flags |= F_EXT_OBS;
         break;
       }
-      Obs o;
-      decide_observe(v, o, true);
       decide_apply(v, o, act, d);
       v.flags &= ~F_EXT_OBS;
       v.flags |= F_INFLIGHT;

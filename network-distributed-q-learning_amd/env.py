@@ -83,10 +83,10 @@ class ASyncSwitchEnv:
     # ---- the AEC protocol, env 0 of an external-action batch (switch_env.py:93, 616-675) ----------------
     def reset(self, seed: Optional[int] = None, options=None, lib=None):
         """Start an episode (switch_env.py:93-158) and run to its first decision.  A new seed (the
-        malfunction stream's, like rail_env.reset(random_seed=seed)) or a reset in the middle of an
-        episode starts a fresh device env; otherwise the env continues into its next episode (the trains'
-        previous / source ports carry over, as in the reference)."""
-        from .aec import AECBatch
+        malfunction stream's, like rail_env.reset(random_seed=seed)) starts a fresh device env; otherwise the
+        env runs the same reset whether its episode ended or not (ACTION_RESET in the middle of one) and the
+        trains' previous / source ports carry over, as in the reference."""
+        from .aec import AECBatch, ACTION_RESET
         import time
         t0 = time.time()
         seed = int(seed if seed is not None else (self.seed if self.seed is not None else 0))
@@ -100,9 +100,7 @@ class ASyncSwitchEnv:
             out = self._aec.step(None)
         else:
             out = self._aec.out
-            if out["agent"][0] >= 0:  # mid-episode: a fresh env
-                self._aec.lib.check(self._aec.lib.dll.sfl_env_begin(self._aec.batch.h), "sfl_env_begin")
-            out = self._aec.step(None)
+            out = self._aec.step([ACTION_RESET] if out["agent"][0] >= 0 else None)
         self.terminated = self.truncated = False
         self._pending()
         self.reset_time += time.time() - t0

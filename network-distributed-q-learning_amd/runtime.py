@@ -166,7 +166,11 @@ class Batch:
             a.trace, a.trace_n = _ptr(tr, C.c_uint64), _ptr(tn, C.c_uint64)
             a.trace_env, a.trace_cap = int(self.trace_env), int(self.trace_cap)
         self.lib.check(fn(self.h, C.byref(a)), fn.__name__)
-        self.timed_kernel_ms += self.counters()["last_kernel_ms"]
+        cnt = self.counters()
+        if tr is None and cnt["kernel_variant"] > 0:
+            # only the phase-timed instantiation stamps phase cycles: a traced launch (the TRACE kernel) or the
+            # lane-per-env body adds kernel time without cycles, which would inflate phase_seconds
+            self.timed_kernel_ms += cnt["last_kernel_ms"]
         if tr is not None:
             self.last_trace = tr[:min(int(tn[0]), self.trace_cap)]
         for k in list(out):

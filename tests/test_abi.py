@@ -164,3 +164,21 @@ def test_experiment_switch_needs_the_experiment_build():
     r = subprocess.run(["g++", "-std=c++17", "-fsyntax-only", "-x", "c++", "-DSFL_X_NOTICK", "-DSFL_EXPERIMENT", hdr],
                        capture_output=True)
     assert r.returncode == 0, r.stderr
+
+
+def test_flags_only_build_is_an_experiment_named_by_its_flags(tmp_path):
+    """a build with extra compiler flags and no defines records its flags, is refused as the product
+    library and accepted (reported by its flags) when experiments are allowed; its id is recomputed from both."""
+    path = build.build_hostsim(out_dir=str(tmp_path), flags=["-fno-unroll-loops"])
+    assert build.built_defines(path) == "" and build.built_flags(path) == "-fno-unroll-loops"
+    lib = _lib.Lib(path)
+    with pytest.raises(_lib.SflError, match="flags: -fno-unroll-loops"):
+        lib.check_fresh()
+    lib.check_fresh(allow_experimental=True)
+    assert lib.experimental and lib.flags == "-fno-unroll-loops" and lib.defines == ""
+    assert lib.build_id == build.build_id([], ["-fno-unroll-loops"])
+
+
+def test_product_library_carries_no_flags():
+    assert build.built_flags(build.build_hip()) == ""
+    assert build.built_flags(build.build_hostsim()) == ""

@@ -65,3 +65,79 @@ def test_learn_mode_refused_after_env_begin():
     with pytest.raises(_lib.SflError, match="external-action"):
         b.batch.step(10)
     b.close()
+
+
+def test_out_of_range_action_is_refused():
+    """an action outside the deciding switch's action space never reaches the env.  AECBatch.step
+    raises before the call; sent straight through the C-ABI, the library reports E_BAD_ACTION and emits the
+    same observation again, with the env's state untouched (no table read past the switch's routes)."""
+    g = _golden.load("c2_mf")
+    cm = comp.compile_scenario(g["scenario_obj"])
+    _lib = importlib.import_module("network-distributed-q-learning_amd._lib")
+    parity = importlib.import_module("network-distributed-q-learning_amd.parity")
+    b = aec.AECBatch(cm, [5, 6], lib=hostsim.lib())
+    out = b.step(None)
+    s0 = int(out["agent"][0])
+    na = int(cm.n_actions[s0])
+    with pytest.raises(ValueError, match="outside switch"):
+        b.step([na, -1])
+    before = {k: np.array(v) for k, v in out.items()}
+    st0 = [np.array(x) for x in parity.env_state(b.batch, 0)]
+    for bad in (na, 7, 200):
+        b._act[:] = [bad, -1]
+        b._io.actions = b._act.ctypes.data_as(_lib.P(_lib.C.c_int32))
+        with pytest.raises(_lib.SflError):
+            b.lib.check(b.lib.dll.sfl_env_step(b.batch.h, _lib.C.byref(b._io)), "sfl_env_step")
+        for k in ("agent", "train", "slot", "state", "mask", "reward", "now"):
+            assert out[k][0] == before[k][0], (bad, k)
+        assert out["next_switch"][0] == -1 and out["step_now"][0] == -1
+        for x, y in zip(parity.env_state(b.batch, 0), st0):
+            assert np.array_equal(np.array(x), y), bad
+    b.close()
+
+
+def test_mid_episode_reset_is_the_reference_reset():
+    """env.reset() in the middle of an episode runs the same reset as at an episode end
+    (switch_env.py:93-158: the trains' previous / source ports carry over), compared with the oracle env
+    driven by the same policy through the same mid-episode resets."""
+    so = importlib.import_module("oracle.sfl_oracle")
+    env_mod = importlib.import_module("network-distributed-q-learning_amd.env")
+    g = _golden.load("c2_mf")
+    sc = g["scenario_obj"]
+    seed = 21
+    oenv, _ = so.build(sc, seed, dict(gamma=1.0, epsilon=0.0, epsilon_decay_rate=1.0, lr=0.1, lr_decay_rate=1.0,
+                                      default_q=0.0), trace=False)
+    denv = env_mod.ASyncSwitchEnv(sc, max_steps=100_000)
+
+    def policy(mask, k):
+        return len(mask) - 1 if k % 3 == 2 else int(np.flatnonzero(mask)[0])
+
+    def run(env, is_oracle, lib=None):
+        rec = []
+        k = 0
+        for n_steps in (17, 5, 40):  # reset, then n decisions, reset again mid-episode ...
+            if is_oracle:
+                env.reset(seed)
+            else:
+                env.reset(seed=seed, lib=lib if k == 0 else None)
+            it = env.agent_iter()
+            for _ in range(n_steps):
+                agent = next(it, None)
+                if agent is None:
+                    break
+                obs, rew, term, trunc, info = env.last()
+                h = env.active_train
+                mask = info["action_mask"]
+                rec.append((agent, h, [int(x) for x in obs], float(rew[h]), [int(x) for x in mask]))
+                post = env.step(policy(mask, k))
+                nxt = post["next_switch"]
+                rec.append((tuple(int(x) for x in (so.switch_id(nxt) if isinstance(nxt, str) else nxt)),
+                            list(post["arrived_trains"])))
+                k += 1
+        return rec
+
+    want = run(oenv, True)
+    got = run(denv, False, hostsim.lib())
+    denv.close()
+    assert len(want) > 100
+    assert got == want
