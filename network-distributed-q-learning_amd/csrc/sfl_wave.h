@@ -37,20 +37,8 @@ namespace wave {
 #ifndef SFL_PF_RING64
 #define SFL_PF_RING64 16  // one env per wavefront with two train slots per lane (c5, k_wave2): see WEnv::RING
 #endif
-#ifndef SFL_LATE_STORES
-// run_groups: the post step's global writes are buffered in LDS and issued at the end of the loop
-// iteration, after the next decision's loads (vmcnt counts stores too: a load issued after them waits for
-// their acknowledgements); a load that may read a buffered address flushes first (see flush_stores)
-#define SFL_LATE_STORES 0
-#endif
 #ifndef SFL_TICK_HOLD
 #define SFL_TICK_HOLD 2  // run_groups: ticks wait while this many groups of the wave can still decide
-#endif
-#ifndef SFL_LOAD_BATCH
-#define SFL_LOAD_BATCH 1  // WEnv::load issues every state load before using any (0: per-record conditional loads)
-#endif
-#ifndef SFL_TICK_HOIST
-#define SFL_TICK_HOIST 1  // tick: the train slots' move-table loads issued together (+0.6 %, profiles/r03_ab_regalloc.txt)
 #endif
 #ifndef SFL_TICK_REMMIN
 #define SFL_TICK_REMMIN 5  // ... and one of them has fewer than this many decisions left (0: hold regardless)
@@ -83,13 +71,7 @@ constexpr uint32_t PF_NONE = 0xFFFFFFFFu;
 // (reward of STOP), if it moves with final rail action 1..3 (reward of a route), and the row's
 // argmax | first allowed argmax << 8 under the staged observation (the row's columns themselves are
 // not kept: a decision on a staged row needs only its max and argmaxes)
-#ifdef SFL_EPS_STAGE
-// doubles and 32-bit words of a prefetch record (stored apart: [TW][PF_D] and [TW][PF_WI]); double 3: the
-// decision's epsilon, staged for its switch's count at the prefetch (-1: none)
-constexpr int PF_D = 4, PF_WI = 3;
-#else
 constexpr int PF_D = 3, PF_WI = 3;  // doubles and 32-bit words of a prefetch record (stored apart: [TW][3] each)
-#endif
 constexpr int PF_WORDS = 2 * PF_D + PF_WI;
 // (doubles: pending cell value, slot word, row max; words: 0 distance at the cell | along the STOP
 // plan << 16, 1 route final action 1 | 2 << 16, 2 route final action 3 | argmax pack << 16 (int16
@@ -352,10 +334,6 @@ struct WEnv {
   // the epsilon-greedy stream (numpy PCG64 state, increment, buffered half) lives in LDS: it is
   // touched once per decision and would otherwise hold ten registers across the whole loop
   uint64_t* lrng;  // [6]: state hi, lo, inc hi, lo, has << 32 | buf
-  // SFL_LATE_STORES (G < 64): the post step's buffered global writes -- u64 values [3] (Q cell, slot words),
-  // u32 offsets [5] (Q cell, slot A, slot B, key-set rows pend / cur), u32 valid bits
-  static constexpr bool LATE = SFL_LATE_STORES && G < 64 && !PART;
-  uint32_t* lsb = nullptr;
   int64_t cum;     // cumulative reward: a sum of integer rewards, exact in f64 (converted on store)
   int32_t n_mf, ep_dec, ep_ticks;
   int32_t step_ctr;
@@ -395,7 +373,6 @@ struct WEnv {
     }
     lpi = (uint32_t*)(lpf + PF_SLOTS * PF_D);
     lrng = (uint64_t*)(lds + G * (PPL + SPL) + PF_SLOTS * PF_WORDS);
-    if constexpr (LATE) lsb = lds + G * (PPL + SPL) + PF_SLOTS * PF_WORDS + 12;
     // PART: the timetable rows are read from the map (L2-resident): a launch runs one or two
     // decisions, so a per-launch LDS copy would cost more than it saves
     if constexpr (PART) ltt = m.tr_pack;
@@ -755,7 +732,6 @@ struct WEnv {
 
   // ---- launch-boundary state transfer ---------------------------------------------------------
   __device__ __forceinline__ void load() {
-#if SFL_LOAD_BATCH
     // every per-lane load is issued unconditionally (clamped index) before any result is used: as conditional
     // loads each sat in its own exec-masked block and waited for its own HBM round trip (16 + 4 + 2 x 8 in a
     // row for c5's partitioned local step, which loads the state every round)
@@ -810,47 +786,7 @@ struct WEnv {
     for (int k = 0; k < SPL; ++k) {
       const uint32_t n = k * G + lane < m.S ? nw[k] : 0u;
       lcnt[k * G + lane] = n;
-
     }
-#else
-#pragma unroll
-    for (int k = 0; k < TPL; ++k) {
-      const int hk = lane + G * k;
-      if (mine[k]) {
-        pos[k] = ld(s.tr_pos, tix(hk));
-        bits[k] = ld(s.tr_bits, tix(hk));
-        plan[k] = ld(s.tr_plan, tix(hk));
-        nprv[k] = (uint32_t)ld(s.tr_next, tix(hk)) | ((uint32_t)ld(s.tr_prev, tix(hk)) << 16);
-        sdec[k] = (uint32_t)ld(s.tr_src, tix(hk)) | ((uint32_t)ld(s.tr_dec, tix(hk)) << 16);
-        delay[k] = ld(s.tr_delay, tix(hk));
-        if constexpr (!PART) {
-          *(vec_t<int32_t, 4>*)(ltt + 8 * hk) = ld((const vec_t<int32_t, 4>*)m.tr_pack, (size_t)hk * 2u);
-          *(vec_t<int32_t, 4>*)(ltt + 8 * hk + 4) = ld((const vec_t<int32_t, 4>*)m.tr_pack, (size_t)hk * 2u + 1u);
-        }
-      } else {
-        pos[k] = -1;
-        bits[k] = 0;
-        plan[k] = 0;
-        nprv[k] = 0xFFFFFFFFu;
-        sdec[k] = 0xFFFFFFFFu;
-        delay[k] = 0;
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < PPL; ++k) {
-      const int p = k * G + lane;
-      const uint32_t r = p < m.NP ? ld(sem_words(), pix(p)) : 0u;
-      sem(k) = r;
-      if constexpr (PART) lsem0[k * G + lane] = r;
-    }
-#pragma unroll
-    for (int k = 0; k < SPL; ++k) {
-      const int sw = k * G + lane;
-      const uint32_t n = sw < m.S ? ld(s.counts, cix(sw)) : 0u;
-      lcnt[k * G + lane] = n;
-
-    }
-#endif
     if constexpr (PART) {
       if (lane < 2 * SPL) ldirty[lane] = 0u;
     }
@@ -1010,7 +946,6 @@ struct WEnv {
       tt1[k] = *(const vec_t<int32_t, 4>*)(ltt + 8 * (mine_(k) ? lid() + G * k : 0) + 4);
     }
     // pass 1: plan pop + prediction, malfunction draw, action preprocessing, desired move
-#if SFL_TICK_HOIST
     // (the slots' move-table rows loaded together, clamped: inside each slot's exec-masked block the
     // second load waited for the first slot's work)
     u4 mrows[TPL];
@@ -1021,7 +956,6 @@ struct WEnv {
       const int pd = pos[k] >= 0 ? (int)tb_dir(bits[k]) : (int)((uint32_t)tt1[k][3] & 0xFFu);
       mrows[k] = ld((const u4*)m.move_tab, (size_t)((uint32_t)(ok ? pc : 0) * 4u + (uint32_t)(ok ? pd : 0)));
     }
-#endif
     bool mover[TPL];
     int32_t desired[TPL], pred[TPL];
     uint32_t aux[TPL];
@@ -1043,11 +977,7 @@ struct WEnv {
         // every check_action of this pass is at (pc, pd): one 16-byte load of the move-table row
         const int pc = p0 >= 0 ? p0 : t_init_cell;
         const int pd = p0 >= 0 ? (int)dir : (int)t_init_dir;
-#if SFL_TICK_HOIST
         const u4 mrow = mrows[k];
-#else
-        const u4 mrow = ld((const u4*)m.move_tab, (size_t)((uint32_t)pc * 4u + (uint32_t)pd));
-#endif
         auto mv_of = [&](uint32_t a) -> Move {
           const uint32_t q = a & 3u;
           return unpack_move(q == 0 ? mrow[0] : q == 1 ? mrow[1] : q == 2 ? mrow[2] : mrow[3]);
@@ -1293,7 +1223,6 @@ struct WEnv {
     mf_mask = MF;
     SFL_LAP(14);
     // _check_active_switch (switch_env.py:427-485)
-#if SFL_TICK_HOIST
     Move amv[TPL];
 #pragma unroll
     for (int k = 0; k < TPL; ++k) {
@@ -1301,19 +1230,13 @@ struct WEnv {
       const uint32_t nxt = pl_len(plan[k]) ? pl_front(plan[k]) : A_FWD;
       amv[k] = check_action<false>(nxt, ok ? pos[k] : 0, ok ? (int)tb_dir(bits[k]) : 0);
     }
-#endif
     bool act[TPL];
 #pragma unroll
     for (int k = 0; k < TPL; ++k) {
       act[k] = false;
       const uint32_t st4 = tb_state(bits[k]);
       if (mine_(k) && pos[k] >= 0 && st4 != S_WAITING) {
-#if SFL_TICK_HOIST
         const Move mv = amv[k];
-#else
-        const uint32_t nxt = pl_len(plan[k]) ? pl_front(plan[k]) : A_FWD;
-        const Move mv = check_action<false>(nxt, pos[k], (int)tb_dir(bits[k]));
-#endif
         if (mv.cell >= 0) {
           const int sw_at = dest_sw(mv);
           if (sw_at >= 0) {
@@ -1347,24 +1270,7 @@ struct WEnv {
   // (after the batch's earlier decisions changed the semaphores) is the staged one, and staged
   // Q values are dropped when the batch writes their cell (pf_written).  Slot words are never
   // stale: a decision writes only its own train's slots and a train decides once per batch.
-  // issue the buffered writes of the last post step (LATE): lanes 0-2 the 8-byte stores, lanes 3-4 the
-  // key-set inserts, one instruction each
-  __device__ __forceinline__ void flush_stores() {
-    if constexpr (LATE) {
-      const uint32_t vm = lsb[11];
-      if (vm) {
-        const int l = lid();
-        const uint32_t off = lsb[6 + (l < 5 ? l : 0)];
-        const uint64_t val = ((const uint64_t*)lsb)[l < 3 ? l : 0];
-        const bool on = l < 5 && ((vm >> l) & 1u);
-        if (on && l < 3) st(l == 0 ? (uint64_t*)qbase() : sbase(), (size_t)off, val);
-        if (on && l >= 3) touch_row(off);
-        lsb[11] = 0u;  // uniform value from every lane
-      }
-    }
-  }
   __device__ __forceinline__ void prefetch(bool greedy) {
-    flush_stores();  // (the staging reads slot words and Q cells the buffered writes may hit)
     const Mask malf = malf_mask();
 #pragma unroll
     for (int k = 0; k < TPL; ++k) pf_roff[k] = pf_qoff[k] = PF_NONE;
@@ -1374,14 +1280,7 @@ struct WEnv {
     // does not survive the launch): stage that train only
     const int h_first = PART ? mctz(q_mask) : -1;
     pf_n = 0;
-#ifdef SFL_EPS_STAGE
-    lrng[5] = 0ull;  // switches decided on since this staging (their staged epsilons are stale)
-#endif
-#ifdef SFL_PF_UNROLL
-#pragma unroll
-#else
 #pragma unroll 1
-#endif
     for (int k = 0; k < TPL; ++k) {
       if (!mbit(q_mask, lid() + G * k)) continue;
       if (PART && lid() + G * k != h_first) continue;
@@ -1432,13 +1331,6 @@ struct WEnv {
     const vec_t<uint32_t, 2> nbw = sw_nb_v(sw);
     const vec_t<int32_t, 4> trw = *(const vec_t<int32_t, 4>*)(ltt + 8 * hk);  // ed, la, k, target
     const u4 pr = port_v(4 * sw + slot);
-#ifdef SFL_EPS_STAGE
-    // epsilon of the decision for its switch's count as it stands (distr_q.py:59-68), a level-1 load; the
-    // decision uses it unless an earlier decision since the staging was on the same switch (lrng[5])
-    const uint32_t n_sw = cget_var(sw);
-    const double eps_h = (greedy || PART || n_sw >= (uint32_t)m.ntab) ? -1.0
-                         : (xp::kEpsConst ? m.eps0 : ld(m.eps_tab, (size_t)(n_sw < (uint32_t)m.ntab ? n_sw : 0u)));
-#endif
     const uint32_t n_plan = pl_len(plan_k);
     const uint32_t a1 = n_plan ? pl_front(plan_k) : A_FWD;
     // move-table rows (all four rail actions) at the cell and after the first rail action
@@ -1551,9 +1443,6 @@ struct WEnv {
     }
     pfl[0] = qv;
     pfl[1] = __longlong_as_double((long long)slw);
-#ifdef SFL_EPS_STAGE
-    pfl[3] = eps_h;
-#endif
     pfi[0] = d16(dd) | (d16(d_stop) << 16);
     pfi[1] = d16(d_rt[1]) | (d16(d_rt[2]) << 16);
     roff_out = (row_ok && !PART) ? roff : PF_NONE;
@@ -1683,7 +1572,6 @@ struct WEnv {
     if (row_hit) {
       SFL_PCNT(4);
     } else if (loc) {
-      flush_stores();
       v_c = ld(qbase() + roff, (size_t)(colv ? lid() : 0));
       SFL_PCNT(5);
     }
@@ -1706,7 +1594,6 @@ struct WEnv {
         q_pend_v = pf_qp;
         SFL_PCNT(6);
       } else {
-        flush_stores();
         q_pend_v = ld(qbase(), (size_t)d.qoff_pend);
         SFL_PCNT(7);
       }
@@ -1728,19 +1615,8 @@ struct WEnv {
       rng.buf = (uint32_t)rng_w[4];
       const uint32_t n = n_sw;
       // eps0 * decay**n (distr_q.py:59-68): host-computed table (a scalar load, K$-resident), pow beyond it
-#ifdef SFL_EPS_STAGE
-      // (read here, not with the decision's first LDS reads: held across the observation they spilled)
-      const double eps_st = pfh[3];
-      const uint64_t eps_dirty = lrng[5];
-      const bool st_ok = !PART && Ud(eps_st) >= 0.0 && !((U(eps_dirty) >> (sw & 63)) & 1ull);
-      if (!PART && !observe_only) lrng[5] = eps_dirty | (1ull << (sw & 63));  // uniform value from every lane
-      const double eps = st_ok ? Ud(eps_st)
-                         : xp::kEpsConst ? m.eps0
-                         : n < (uint32_t)m.ntab ? LDC(m.eps_tab, (size_t)n) : m.eps0 * pow_ool(m.eps_decay, (double)n);
-#else
       const double eps = xp::kEpsConst ? m.eps0
                          : n < (uint32_t)m.ntab ? LDC(m.eps_tab, (size_t)n) : m.eps0 * pow_ool(m.eps_decay, (double)n);
-#endif
       explore = Ud(pcg_double(rng)) < eps;
       if (explore && !observe_only) {
         const uint32_t sub_seed = pcg_bounded(rng, 2147483646u);
@@ -2007,34 +1883,6 @@ struct WEnv {
     }
     // every global write of the step from one lane-0 region
     // (xp::kNo*: timing-only experiment builds that drop one class of store, sfl_experiment.h)
-    if constexpr (LATE && !xp::kNoQStore && !xp::kNoTouch && !xp::kNoSlot) {
-      // buffered (flush_stores): uniform values, written by every lane
-      ((uint64_t*)lsb)[0] = (uint64_t)__double_as_longlong(nv);
-      ((uint64_t*)lsb)[1] = slot_make(PEND_NONE, slot_rew(d.slotword, epoch), epoch);
-      ((uint64_t*)lsb)[2] = slot_make(pend_make((uint32_t)d.sw, (uint32_t)d.slot, d.state, (uint32_t)d.j), d.r_new, epoch);
-      lsb[6] = d.qoff_pend;
-      lsb[7] = slot_ix(d.sw, d.h);
-      lsb[8] = slot_ix(d.next_sw, d.h);
-      lsb[9] = d.row_pend;
-      lsb[10] = d.row_cur;
-      // (slot B replaces slot A when the train stays at its switch: one lane per address)
-      lsb[11] = (hp ? 9u : 0u) | ((hp && d.next_sw != d.sw) ? 2u : 0u) | 4u | ((d.touch_cur || (hp && d.sw != ps)) ? 16u : 0u);
-    } else
-#ifdef SFL_POST_LANES
-    // the step's global writes as two instructions over five lanes of the group: lanes 0-2 the 8-byte
-    // stores (the pending update's Q cell, the two slot words), lanes 3-4 the key-set inserts
-    if constexpr (!xp::kNoQStore && !xp::kNoTouch && !xp::kNoSlot) {
-      const int l = lid();
-      const uint64_t sa = slot_make(PEND_NONE, slot_rew(d.slotword, epoch), epoch);
-      const uint64_t sb = slot_make(pend_make((uint32_t)d.sw, (uint32_t)d.slot, d.state, (uint32_t)d.j), d.r_new, epoch);
-      const size_t off = l == 0 ? (size_t)d.qoff_pend : (size_t)slot_ix(l == 1 ? d.sw : d.next_sw, d.h);
-      uint64_t* base = l == 0 ? (uint64_t*)qbase() : sbase();
-      const uint64_t val = l == 0 ? (uint64_t)__double_as_longlong(nv) : (l == 1 ? sa : sb);
-      if ((l == 0 && hp) || l == 1 || l == 2) st(base, off, val);
-      const bool ins = (l == 3 && hp) || (l == 4 && (d.touch_cur || (hp && d.sw != ps)));
-      if (ins) touch_row(l == 3 ? d.row_pend : d.row_cur);
-    } else
-#endif
     if (lid() == 0) {
       if (hp) {
         if (!xp::kNoQStore) st(qbase(), (size_t)d.qoff_pend, nv);
@@ -2053,10 +1901,7 @@ struct WEnv {
     // same successor switch => same slot), so the lanes' updates are independent.
     Mask fresh = arr_mask & ~fl_mask;
     fl_mask |= fresh;
-    if (many(fresh)) {
-      pf_ok = false;  // bonus writes: stage the rest of the batch again
-      flush_stores();  // (the bonus reads slot words and Q cells the buffered writes may hit)
-    }
+    if (many(fresh)) pf_ok = false;  // bonus writes: stage the rest of the batch again
     while (many(fresh)) {
       const int tr = mctz(fresh);
       mclear_low(fresh);
@@ -2453,7 +2298,7 @@ __device__ void run_groups(const SflMap& m, const SflState& s, const SflCtl& c) 
   // per env: semaphores, counters, prefetch records, rng; per block: the timetable rows and the
   // per-switch / per-port map records (the groups of a wave read different switches' records: LDS
   // reads instead of vector loads)
-  constexpr int LDS_WORDS = (G * (PPL + SPL) + V::PF_SLOTS * PF_WORDS + 12 + (V::LATE ? 12 : 0) + 3) / 4 * 4;
+  constexpr int LDS_WORDS = (G * (PPL + SPL) + V::PF_SLOTS * PF_WORDS + 12 + 3) / 4 * 4;
   constexpr int EPB = SFL_GROUP_BLOCK / G;  // envs per block (sfl.hip launches)
   constexpr int SWX = G * SPL, NPX = G * PPL;  // switches / ports the shape holds
   constexpr int O_TT = EPB * LDS_WORDS, O_SW = O_TT + TW * 8, O_PP = O_SW + SWX * V::SW_LDS, O_PT = O_PP + NPX * 4;
@@ -2473,7 +2318,6 @@ __device__ void run_groups(const SflMap& m, const SflState& s, const SflCtl& c) 
   v.tpt = lds + O_PT;
   PhaseTimer tm;
   if constexpr (TIMED) tm.start(c.phase_cyc != nullptr && blockIdx.x % TM_SAMPLE == 0u && threadIdx.x < 64u);
-  if constexpr (V::LATE) v.lsb[11] = 0u;
   v.load();
   int32_t phase = ld(s.phase, e);
   int32_t ep_t = ld(s.ep_t, e), n_test = ld(s.n_test, e);
@@ -2527,7 +2371,6 @@ __device__ void run_groups(const SflMap& m, const SflState& s, const SflCtl& c) 
       phase = PH_TICK;
     }
     if constexpr (TIMED) tm.lap(TM_RESET);
-#ifndef SFL_GROUP_NOSYNC
     // the groups waiting for a tick start it once fewer than SFL_TICK_HOLD groups can still
     // decide: their ticks then run together, while the last deciding group (if any) runs its
     // batch alongside.  Measured at G = 16 (c3): hold while >= 2 decide 1,316 M, while >= 1
@@ -2542,9 +2385,6 @@ __device__ void run_groups(const SflMap& m, const SflState& s, const SflCtl& c) 
     const bool dec_ph = phase == PH_POST || phase == PH_DECIDE;
     const bool wave_decides = (int)__builtin_popcountll(__ballot(dec_ph)) >= SFL_TICK_HOLD * G &&
                               (SFL_TICK_REMMIN <= 0 || __ballot(dec_ph && mpopc(v.q_mask) < SFL_TICK_REMMIN) != 0ull);
-#else
-    const bool wave_decides = false;
-#endif
 #ifdef SFL_PROFILE
     tp0 = __builtin_amdgcn_s_memtime();
 #endif
@@ -2646,9 +2486,7 @@ __device__ void run_groups(const SflMap& m, const SflState& s, const SflCtl& c) 
       }
       phase = PH_RESET;
     }
-    v.flush_stores();  // LATE: the iteration's post writes, after its decision's loads
   }
-  v.flush_stores();
   v.store(phase);
   if constexpr (TIMED) tm.flush(c);
 #ifdef SFL_PROFILE
