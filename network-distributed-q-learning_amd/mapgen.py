@@ -626,7 +626,7 @@ CITY_MARGIN = 7
 def from_flatland_params(width: int, height: int, max_num_cities: int, number_of_agents: int, seed: int,
                          malfunction=(0.0, 0, 0), spacing: int = 5, margin: int = 3,
                          max_rails_between_cities: Optional[int] = None,
-                         max_rail_pairs_in_city: Optional[int] = None) -> Scenario:
+                         max_rail_pairs_in_city: Optional[int] = None, layout: str = "auto") -> Scenario:
     """Scenario for the reference's [ENV] config keys (main.py:21-60) on a width x height grid.
 
     Flatland's sparse_rail_generator is absent, so this is a stand-in layout, not its output (parity
@@ -638,7 +638,13 @@ def from_flatland_params(width: int, height: int, max_num_cities: int, number_of
     ``max_rails_between_cities`` >= 2 gives every backbone segment without a city a passing loop (two rails
     between its junctions; a city's segment has its own parallel tracks); ``max_rail_pairs_in_city`` = k gives
     each city 2 * randint(1, k + 1) tracks, as Flatland draws them.  Left out (None), the round-2 layout:
-    single-track backbone, 2-3 tracks per city."""
+    single-track backbone, 2-3 tracks per city.
+
+    Round 4: with ``max_rails_between_cities`` given, the cities are joined as Flatland joins them -- each link
+    between neighbouring cities a rail path of its own (``max_rails_between_cities`` of them, at most two),
+    switches only at the cities -- on a lattice of as many cities as fit the grid, up to ``max_num_cities``
+    (``generate_city_grid``).  ``layout="backbone"`` keeps the round-3 layout (cities on a square backbone of
+    shared four-way junctions, a passing loop per segment) for the fixtures recorded on it."""
     import warnings
     size = max(int(width), int(height))
     n_cities, n_agents = int(max_num_cities), int(number_of_agents)
@@ -649,8 +655,25 @@ def from_flatland_params(width: int, height: int, max_num_cities: int, number_of
         choices = [2 * k for k in range(1, max(1, int(max_rail_pairs_in_city)) + 1)]
         spacing_need = max(CITY_SPACING if max(choices) <= 3 else 0, 4 * max(choices) + 4)
     if rails > 2:
-        warnings.warn(f"max_rails_between_cities={rails}: the stand-in layout lays at most two rails per segment",
+        warnings.warn(f"max_rails_between_cities={rails}: the stand-in layout lays at most two rails per link",
                       stacklevel=2)
+    if layout not in ("auto", "backbone"):
+        raise ValueError(f"layout {layout!r}: 'auto' or 'backbone'")
+    if max_rails_between_cities is not None and n_cities >= 2 and layout == "auto":
+        # round 4: Flatland's way of joining cities -- every link between two neighbouring cities a rail path of
+        # its own, switches only at the cities (generate_city_grid); as many cities as fit the grid, up to
+        # max_num_cities (Flatland places cities until it runs out of room or reaches the cap)
+        pairs = int(max_rail_pairs_in_city) if max_rail_pairs_in_city is not None else 1
+        tracks = [2 * k for k in range(1, max(1, pairs) + 1)]
+        r_fit, c_fit = city_grid_fit(size, max(tracks))
+        if r_fit * c_fit >= 2:
+            cols = min(c_fit, max(1, n_cities))
+            rows = min(r_fit, max(1, n_cities // cols))
+            if rows * cols < 2:
+                rows, cols = min(r_fit, 2), 1
+            return generate_city_grid(rows, cols, n_agents, seed=int(seed), track_choices=tracks,
+                                      rails=min(max(rails, 1), 2), size=size, malfunction=malfunction,
+                                      name=f"flatland_{width}x{height}")
     n_fit = (size - 2 * CITY_MARGIN - 1) // spacing_need + 1  # backbone lines that fit the grid
     if n_cities >= 2 and n_fit >= 3:  # (a two-line backbone is a loop a train cannot turn around on)
         n_lines = 3
@@ -669,3 +692,178 @@ def from_flatland_params(width: int, height: int, max_num_cities: int, number_of
     return generate(n_switches=n_sw, n_trains=n_agents, n_stations=max(1, min(n_cities, n_agents)), seed=int(seed),
                     nx_lines=n_lines, ny_lines=n_lines, spacing=spacing, margin=margin, size=size,
                     malfunction=malfunction, name=f"flatland_{width}x{height}")
+
+
+# ---------------------------------------------------------------------------
+# Flatland-like city graph (round 4): cities joined by their own rail paths
+# ---------------------------------------------------------------------------
+
+def city_grid_network(n_rows: int, n_cols: int, tracks: List[List[int]], *, plat: int = 6, margin: int = 2,
+                      rails: int = 1, size: Optional[int] = None):
+    """Cities on an ``n_rows`` x ``n_cols`` lattice, joined the way Flatland's sparse_rail_generator joins them --
+    each link between two neighbouring cities is a rail path of its own, and switches sit at the cities (there is
+    no shared junction between links):
+
+    * city (i, j) has ``tracks[i][j]`` parallel platform tracks; the first lies on its row's main line, the others
+      below it, each joined to the main line at both ends of the platforms by a T switch whose trunk faces out of
+      the city (a throat, as in ``city_network``);
+    * the cities of a row are joined by that main line (west-east links); its two ends turn into a return track two
+      rows above, and a chord near each end joins the two (T switches), so a train can turn round on its row;
+    * city (i, j) is joined to city (i + 1, j) by ``rails`` vertical rail paths (Flatland's
+      max_rails_between_cities) on the east side of both cities: each leaves the upper city's main line at a T
+      switch (trunk facing the city) and enters the lower city's main line at another (trunk facing the city), so
+      a train leaving either city eastwards may take it and arrives heading into the other city; a path crossing
+      the lower row's return track does so at a diamond crossing (no switching).
+
+    Returns (grid, junction cells, per-city track cells, per-city (row, platform span))."""
+    Pm = max(max(r) for r in tracks)
+    tw = 2 * Pm - 1                 # a throat's extent beyond the platform span
+    # per link column pair: rows i even use columns +2 / +4, rows i odd +6 / +8 past the city's east throat
+    foot = 2 * tw + plat + 1         # a city's span on its row, throats included
+    sp_c = foot + 12                 # + its east links (2 columns) and the next city's west links (2), with gaps
+    sp_r = 2 * (Pm - 1) + 4
+    xL = margin
+    R0 = margin + 2
+    xR = xL + 10 + (n_cols - 1) * sp_c + foot + 8
+    rows = [R0 + i * sp_r for i in range(n_rows)]
+    side = max(size or 0, xR + margin + 1, rows[-1] + 2 * (Pm - 1) + margin + 1)
+    if rows[-1] + 2 * (Pm - 1) > side - 1 or xR > side - 1:
+        raise ValueError("city grid does not fit")
+    pairs: Dict[Tuple[int, int], Set[FrozenSet[int]]] = {}
+
+    def add(r, c, a, b):
+        pairs.setdefault((r, c), set()).add(frozenset((a, b)))
+
+    junctions: Set[Tuple[int, int]] = set()
+    city_tracks, city_spans = [], []
+    for i, R in enumerate(rows):
+        # the row loop: main line R from xL to xR, return track R - 2, end verticals
+        _straight(R, xL, R, xR, pairs)
+        _straight(R - 2, xL, R - 2, xR, pairs)
+        add(R, xL, E, N)
+        add(R - 1, xL, N, S)
+        add(R - 2, xL, S, E)
+        add(R, xR, W, N)
+        add(R - 1, xR, N, S)
+        add(R - 2, xR, S, W)
+        # a chord near each end, so that a train can turn round on its row: westbound on the main line it may
+        # climb the west chord and come back eastbound (round the west end), eastbound the east chord
+        for xc, tm, tr_ in ((xL + 2, E, W), (xR - 2, W, E)):
+            add(R, xc, tm, N)
+            add(R - 1, xc, N, S)
+            add(R - 2, xc, tr_, S)
+            junctions.update({(R, xc), (R - 2, xc)})
+        for j in range(n_cols):
+            P = int(tracks[i][j])
+            a = xL + 10 + j * sp_c + tw      # platform cells a + 1 .. b - 1
+            b = a + plat + 1
+            trk = [[(R, c) for c in range(a + 1, b)]]
+            for k in range(1, P):
+                rk, xw, xe = R + 2 * k, a - (2 * k - 1), b + (2 * k - 1)
+                add(R, xw, W, S)
+                add(R, xe, E, S)
+                junctions.update({(R, xw), (R, xe)})
+                _straight(R, xw, rk, xw, pairs)
+                _straight(R, xe, rk, xe, pairs)
+                add(rk, xw, N, E)
+                add(rk, xe, N, W)
+                _straight(rk, xw, rk, xe, pairs)
+                trk.append([(rk, c) for c in range(a + 1, b)])
+            city_tracks.append(trk)
+            city_spans.append((R, a, b))
+            if i + 1 < n_rows:
+                R2 = rows[i + 1]
+                for q in range(max(1, int(rails))):
+                    # the first link on the cities' east side, the second on their west side (trunks facing the
+                    # cities: trains leaving a city may take a link, trains off a link head into the city)
+                    east = q % 2 == 0
+                    X = (b + tw + 2 + (2 if i % 2 else 0)) if east else (a - tw - 3 - (2 if i % 2 else 0))
+                    tk = W if east else E
+                    add(R, X, tk, S)
+                    add(R2, X, tk, N)
+                    _straight(R, X, R2, X, pairs)
+                    add(R2 - 2, X, N, S)  # crosses the lower row's return track (diamond)
+                    junctions.update({(R, X), (R2, X), (R2 - 2, X)})
+    grid = np.zeros((side, side), dtype=np.int64)
+    for (r, c), prs in pairs.items():
+        grid[r, c] = pairs_to_bits(prs)
+    return grid, junctions, city_tracks, city_spans
+
+
+def city_grid_fit(size: int, max_tracks: int, plat: int = 6, margin: int = 2) -> Tuple[int, int]:
+    """(rows, columns) of cities ``city_grid_network`` fits into a size x size grid."""
+    tw = 2 * max_tracks - 1
+    foot = 2 * tw + plat + 1
+    sp_c, sp_r = foot + 12, 2 * (max_tracks - 1) + 4
+    cols = 0
+    while margin + 10 + cols * sp_c + foot + 8 + margin + 1 <= size:
+        cols += 1
+    rows = 0
+    while margin + 2 + rows * sp_r + 2 * (max_tracks - 1) + margin + 1 <= size:
+        rows += 1
+    return rows, cols
+
+
+def generate_city_grid(n_rows: int, n_cols: int, n_trains: int, seed: int, *, track_choices: Sequence[int] = (2, 4),
+                       rails: int = 1, plat: int = 6, size: Optional[int] = None,
+                       malfunction: Tuple[float, int, int] = (0.0, 0, 0), name: str = "", max_tries: int = 200) -> Scenario:
+    """Scenario on ``city_grid_network``: one station per city (a platform cell in the middle third of one of its
+    tracks), trains starting on city tracks and targeting another city's station, timetable as
+    flatland_patch/timetable_generators.py (``timetable``).  ``track_choices``: a city's track count is drawn from it
+    (Flatland: 2 * randint(1, max_rail_pairs_in_city + 1))."""
+    n_cities = n_rows * n_cols
+    if n_cities < 2:
+        raise ValueError("at least two cities")
+    rng = np.random.default_rng(seed)
+    for _ in range(max_tries):
+        tracks = [[int(track_choices[int(rng.integers(0, len(track_choices)))]) for _j in range(n_cols)]
+                  for _i in range(n_rows)]
+        grid, junctions, city_tracks, _spans = city_grid_network(n_rows, n_cols, tracks, plat=plat, rails=rails, size=size)
+        if not strongly_connected(grid):
+            continue
+        near_junction = lambda rc: any((rc[0] + dr, rc[1] + dc) in junctions for dr, dc in DELTA)  # noqa: E731
+        stations, pools = [], []
+        for tr in city_tracks:
+            t = tr[int(rng.integers(0, len(tr)))]
+            cells = t[len(t) // 3: 2 * len(t) // 3 + 1]
+            st = cells[int(rng.integers(0, len(cells)))]
+            stations.append(st)
+            pools.append([c for trk in tr for c in trk if c != st and not near_junction(c)])
+        dists = {st: distance_to_cell(grid, st) for st in stations}
+        trains: List[Train] = []
+        used = set()
+        for _k in range(n_trains):
+            placed = False
+            for _try in range(100):
+                home = int(rng.integers(0, n_cities))
+                cand = [c for c in pools[home] if c not in used]
+                if not cand:
+                    continue
+                p0 = cand[int(rng.integers(0, len(cand)))]
+                h0 = (E, W)[int(rng.integers(0, 2))]
+                dest = int(rng.integers(0, n_cities - 1))
+                dest = dest + 1 if dest >= home else dest
+                tgt = stations[dest]
+                if tgt in _first_switch_chain(grid, junctions, p0, h0) or dists[tgt][p0[0], p0[1], h0] < 0:
+                    continue
+                used.add(p0)
+                trains.append(Train((int(p0[0]), int(p0[1])), int(h0), (int(tgt[0]), int(tgt[1]))))
+                placed = True
+                break
+            if not placed:
+                break
+        if len(trains) != n_trains:
+            continue
+        trains.sort(key=lambda t: (t.initial_position[0], t.initial_position[1], t.initial_direction))
+        lens = [int(dists[t.target][t.initial_position[0], t.initial_position[1], t.initial_direction]) + 1
+                for t in trains]
+        Hh, Ww = grid.shape
+        rs = np.random.RandomState(seed & 0x7FFFFFFF)
+        eds, las, mes = timetable(lens, Ww, Hh, n_cities, rs)
+        for t, ed, la in zip(trains, eds, las):
+            t.earliest_departure, t.latest_arrival = ed, la
+        return Scenario(height=Hh, width=Ww, grid=[[int(x) for x in row] for row in grid], trains=trains,
+                        max_episode_steps=int(mes), malfunction_rate=float(malfunction[0]),
+                        malfunction_min=int(malfunction[1]), malfunction_max=int(malfunction[2]),
+                        name=name, seed=int(seed))
+    raise RuntimeError("could not generate a strongly connected city-grid scenario")

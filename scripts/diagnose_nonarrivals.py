@@ -37,6 +37,12 @@ def scenario(mapgen, layout, seed, **kw):
         warnings.simplefilter("ignore")
         if layout == "cities":
             return mapgen.from_flatland_params(80, 80, 25, 15, seed, malfunction=(0.0, 0, 0), **kw)
+        if layout.startswith("citygrid"):  # citygrid[RxC]
+            rc = layout[8:] or "4x2"
+            r, c = (int(x) for x in rc.split("x"))
+            return mapgen.generate_city_grid(r, c, 15, seed, rails=kw.get("max_rails_between_cities", 2),
+                                             track_choices=[2 * k for k in range(1, kw.get("max_rail_pairs_in_city", 2) + 1)],
+                                             size=80)
         return mapgen.generate(60, 15, 8, seed=seed)
 
 

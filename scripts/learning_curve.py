@@ -32,7 +32,9 @@ def main():
     ap.add_argument("--exploit-freq", type=int, default=100)
     ap.add_argument("--chunk", type=int, default=500, help="episodes per learn call (progress lines)")
     ap.add_argument("--host", action="store_true", help="run the host build (tests only)")
-    ap.add_argument("--layout", default="cities", choices=["cities", "grid"],
+    ap.add_argument("--rows", type=int, default=0, help="with --layout citygrid: city rows (0: what fits)")
+    ap.add_argument("--cols", type=int, default=0, help="with --layout citygrid: city columns (0: what fits)")
+    ap.add_argument("--layout", default="cities", choices=["cities", "grid", "citygrid"],
                     help="cities: main.py's [ENV] keys (mapgen.from_flatland_params, city stand-in); grid: a line-grid "
                          "stand-in with the same trains (mapgen.generate, 60 switches, 8 stations)")
     ap.add_argument("--rails", type=int, default=2, help="max_rails_between_cities (the sweep: 2)")
@@ -58,6 +60,9 @@ def main():
                 # the sweep's [ENV] keys (hyperparam_tuning.py:17-25), as main.py passes them
                 sc = mapgen.from_flatland_params(80, 80, 25, 15, seed, malfunction=(0.0, 0, 0),
                                                  max_rails_between_cities=args.rails, max_rail_pairs_in_city=args.pairs)
+            elif args.layout == "citygrid":
+                sc = mapgen.generate_city_grid(args.rows or 4, args.cols or 2, 15, seed, rails=args.rails,
+                                               track_choices=[2 * k for k in range(1, args.pairs + 1)], size=80)
             else:
                 sc = mapgen.generate(60, 15, 8, seed=seed)
         cm = comp.compile_scenario(sc)

@@ -166,7 +166,11 @@ CASES = [
     ("city6_s5", ("cities", 6, 12), 5, (0.02, 3, 8), 2024, HP_DECAY, 10, 3),
     # the sweep config's layout keys (hyperparam_tuning.py:17-25) on a smaller grid: from_flatland_params with
     # max_rails_between_cities = 2 (passing loops on the backbone) and max_rail_pairs_in_city = 2 (2 or 4 tracks)
-    ("citysweep_s5", ("flatland", 60, 6, 8, 2, 2), 5, (0.02, 3, 8), 2024, HP_TEST_MODEL, 10, 3),
+    # -- round 3's layout (layout="backbone")
+    ("citysweep_s5", ("flatland-backbone", 60, 6, 8, 2, 2), 5, (0.02, 3, 8), 2024, HP_TEST_MODEL, 10, 3),
+    # the same keys on round 4's layout: every link between neighbouring cities a rail path of its own
+    # (mapgen.generate_city_grid: five cities on a 60 x 60 grid, two links per neighbouring pair, 2 or 4 tracks)
+    ("citygrid_s5", ("flatland", 60, 6, 8, 2, 2), 5, (0.02, 3, 8), 2024, HP_TEST_MODEL, 10, 3),
 ]
 
 
@@ -177,9 +181,10 @@ def main(only=None):
             continue
         if isinstance(cfg, str):
             sc = mapgen.make_config(cfg, seed=mseed, malfunction=mf)
-        elif cfg[0] == "flatland":
+        elif cfg[0].startswith("flatland"):
             sc = mapgen.from_flatland_params(cfg[1], cfg[1], cfg[2], cfg[3], mseed, malfunction=mf,
-                                             max_rails_between_cities=cfg[4], max_rail_pairs_in_city=cfg[5])
+                                             max_rails_between_cities=cfg[4], max_rail_pairs_in_city=cfg[5],
+                                             layout="backbone" if cfg[0] == "flatland-backbone" else "auto")
         else:
             sc = mapgen.generate_cities(cfg[1], cfg[2], seed=mseed, malfunction=mf, name=name)
         data = run_case(name, sc, seed, hp, neps, exploit_freq=exploit)
