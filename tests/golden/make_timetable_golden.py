@@ -42,7 +42,11 @@ CASES = [
     ("city6", "generate_cities", dict(n_cities=6, n_trains=12, seed=450565)),
     ("city9_s77", "generate_cities", dict(n_cities=9, n_trains=24, seed=77)),
 ] + [(f"sweep80_s{s}", "from_flatland_params", dict(width=80, height=80, max_num_cities=25, number_of_agents=15, seed=s))
-     for s in (64, 65, 66, 67, 69)]  # hyperparam_tuning.py:10-35
+     for s in (64, 65, 66, 67, 69)] + [  # hyperparam_tuning.py:10-35
+    # round 4: the sweep's layout keys (max_rails_between_cities 2, max_rail_pairs_in_city 2) -> generate_city_grid
+    (f"sweepgrid80_s{s}", "from_flatland_params", dict(width=80, height=80, max_num_cities=25, number_of_agents=15, seed=s,
+                                                      max_rails_between_cities=2, max_rail_pairs_in_city=2))
+    for s in (64, 65, 66, 67, 69)]
 
 
 def scenario(gen, kw):
@@ -68,6 +72,11 @@ def n_cities_of(gen, kw, sc):
 
 def _cities_from_params(kw):
     size = max(kw["width"], kw["height"])
+    if kw.get("max_rails_between_cities") is not None:  # generate_city_grid: as many cities as fit, up to the cap
+        pairs = kw.get("max_rail_pairs_in_city") or 1
+        r_fit, c_fit = mapgen.city_grid_fit(size, 2 * pairs)
+        cols = min(c_fit, kw["max_num_cities"])
+        return min(r_fit, max(1, kw["max_num_cities"] // cols)) * cols
     n_fit = (size - 2 * mapgen.CITY_MARGIN - 1) // mapgen.CITY_SPACING + 1
     n_lines = 3
     while n_lines * (n_lines - 1) < kw["max_num_cities"] and n_lines < n_fit:
