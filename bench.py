@@ -452,9 +452,11 @@ def bench_partition(args):
     barrier()
     t0 = time.perf_counter()
     rounds = 0
+    ck0, d0, (w0, r0) = pb.checkpoints, pb.deferrals, pb.sync_count()
     for _ in range(args.steps):
         rounds += pb.step(args.decisions)
     barrier()
+    (w1, r1) = pb.sync_count()
     dt = time.perf_counter() - t0
     total = float(E * args.decisions * args.steps)
     dt, total_all = par.reduce_timing(dist, dt, total, device=red_dev)
@@ -496,6 +498,13 @@ def bench_partition(args):
                        "local_switches": int(pb.local_mask.sum()),
                        "envs_per_gpu": E, "decisions_per_env_per_step": args.decisions,
                        "rounds_per_step": rounds / max(1, args.steps),
+                       # the host's part in the rounds: count reads / device waits of the library (at the
+                       # checkpoints only), the fixed segment sizes the ranks agreed on, envs deferred
+                       "checkpoints_per_step": (pb.checkpoints - ck0) / max(1, args.steps),
+                       "host_waits_per_step": (w1 - w0) / max(1, args.steps),
+                       "count_reads_per_step": (r1 - r0) / max(1, args.steps),
+                       "segment_records": [pb.k_req, pb.k_upd], "segment_capacity": [pb.cap_req, pb.cap_upd],
+                       "deferrals": pb.deferrals - d0,
                        "parallelism": f"env-batch dp{world} x switch-agent partition {world}"},
             "library": library_info(pb.lib),
             "world_size": world,

@@ -179,26 +179,44 @@ int sfl_mf_schedule_flatland(const uint32_t* key, int32_t nkey, const int32_t* w
  * to its last request, runs to its next decision and writes that decision's request, plus the
  * update records of its post step), an all-to-all of the update and request buffers,
  * sfl_part_update + sfl_part_answer on the received records, and an all-to-all of the replies
- * back.  Buffers are [world][cap + 1] records (record 0 of a segment = header holding the
- * count); on the GPU they are device pointers (the caller's RCCL buffers).  Replaces the
- * reference's in-process successor lookup max_q(next_state, next_agent) and update
+ * back.  Buffers are [world][k + 1] records (record 0 of a segment = header holding the count; k =
+ * the capacities of sfl_part_set_caps, the configured ones until then); on the GPU they are device
+ * pointers (the caller's RCCL buffers).  An env whose request or update records do not all fit
+ * this round's segments is deferred whole: it sends nothing (its places below the segment end carry
+ * void records), sits out the next sfl_part_local and sends the same records again -- so the
+ * exchange has a fixed size and needs no counts, and results do not depend on the capacities.
+ * Replaces the reference's in-process successor lookup max_q(next_state, next_agent) and update
  * (switchfl/distr_q.py:419-466) across GPU boundaries. */
 int sfl_part_config(sfl_handle* h, int32_t rank, int32_t world, const int32_t* owner /* [S] */, uint32_t env_base,
                     uint32_t envs_total, uint32_t cap_req /* >= n_envs */, uint32_t cap_upd);
 int sfl_part_record_sizes(uint32_t* req, uint32_t* rep, uint32_t* upd);
 int sfl_part_begin(sfl_handle* h);  /* start a part step: per-env decision counters to 0 */
+/* requests_sent: the envs with a request or deferred this round (null: see sfl_set_stream) */
 int sfl_part_local(sfl_handle* h, int64_t decisions_per_env, const void* replies, void* requests, void* updates,
                    uint64_t* requests_sent /* null: see sfl_set_stream */);
 int sfl_part_update(sfl_handle* h, const void* updates);
 int sfl_part_answer(sfl_handle* h, const void* requests, void* replies);
 /* this rank's record counts of the last sfl_part_local: out[0 .. world) requests and
- * out[world .. 2 world) update records per destination, out[2 world] the highest update stage
- * (cap >= 2 * world + 1); synchronises if sfl_part_local did not (and reports the envs' errors) */
+ * out[world .. 2 world) update records per destination (staged, sent or deferred), out[2 world] the
+ * highest update stage sent; then, when cap allows (4 world + 4 words): out[2 world + 1 .. 3 world + 1)
+ * and out[3 world + 1 .. 4 world + 1) the peaks of those two counts since the previous call,
+ * out[4 world + 1] the envs with a request or deferred, out[4 world + 2] the envs deferred in that
+ * round, out[4 world + 3] the deferrals since the previous call.  cap >= 2 * world + 1;
+ * synchronises if sfl_part_local did not (and reports the envs' errors) */
 int sfl_part_counts(sfl_handle* h, uint32_t* out, int32_t cap);
+/* the segment capacities of the next rounds (records per destination, 1 <= k <= the configured
+ * cap_req / cap_upd): every rank of the job sets the same values, at a point where no round is in
+ * flight (the buffers of a round are [world][k + 1] records).  A smaller k moves fewer bytes per
+ * round; an env that does not fit waits a round (see above). */
+int sfl_part_set_caps(sfl_handle* h, uint32_t k_req, uint32_t k_upd);
+/* how often the handle has waited for its device since create (stream / event synchronisations; 0 on
+ * the host build) and read the round counts back (sfl_part_counts, sfl_part_local with requests_sent):
+ * what a caller checks to see that its rounds queue without the host in the loop */
+int sfl_get_sync_count(sfl_handle* h, uint64_t* waits, uint64_t* count_reads);
 /* queue the handle's work on the caller's stream (a hipStream_t, e.g. torch's current stream,
  * which its RCCL collectives follow).  Then sfl_part_update / sfl_part_answer return without a
  * synchronisation, and so does sfl_part_local when requests_sent is null (its counts are read by
- * sfl_part_counts): a round synchronises once, for the counts, or -- one rank -- not at all.
+ * sfl_part_counts): the rounds between two sfl_part_counts calls queue without a synchronisation.
  * null: the handle's own stream again */
 int sfl_set_stream(sfl_handle* h, void* stream);
 /* Which switches' rows the wave kernel decides on and updates in place: local_switches[S] (1 = in

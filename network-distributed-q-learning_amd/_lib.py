@@ -102,6 +102,8 @@ EXPORTS = {
     "sfl_part_update": (C.c_int, [C.c_void_p, C.c_void_p]),
     "sfl_part_answer": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
     "sfl_part_counts": (C.c_int, [C.c_void_p, P(C.c_uint32), C.c_int32]),
+    "sfl_part_set_caps": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32]),
+    "sfl_get_sync_count": (C.c_int, [C.c_void_p, P(C.c_uint64), P(C.c_uint64)]),
     "sfl_set_stream": (C.c_int, [C.c_void_p, C.c_void_p]),
     "sfl_part_set_local_rows": (C.c_int, [C.c_void_p, P(C.c_uint8)]),
     "sfl_part_get_q": (C.c_int, [C.c_void_p, C.c_uint32, P(C.c_double), P(C.c_uint32)]),

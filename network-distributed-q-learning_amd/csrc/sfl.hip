@@ -55,14 +55,9 @@ __global__ void __launch_bounds__(SFL_WAVE_BLOCK) __attribute__((amdgpu_waves_pe
 // (TW <= G) 4 -- c2 (variant 6): 918 M vs 805 M at 3 (VGPR-bound, spills a little; 5: 589 M) --,
 // two slots per lane 4 with the prefetch ring (SFL_PF_RING: the LDS then allows 4 blocks per CU),
 // 3 without it
-#ifndef SFL_GROUP_OCC1
-#define SFL_GROUP_OCC1 4
-#endif
-#ifndef SFL_GROUP_OCC
-#define SFL_GROUP_OCC (SFL_PF_RING > 0 ? 4 : 3)  // two slots per lane: 4 with the prefetch ring (LDS 4 blocks/CU)
-#endif
-template <int PPL, int SPL, int TW, bool TRACE, int G, bool TIMED = false>
-__global__ void __launch_bounds__(SFL_GROUP_BLOCK) __attribute__((amdgpu_waves_per_eu(TW <= G ? SFL_GROUP_OCC1 : SFL_GROUP_OCC)))
+// (sfl::kVariants[v].OCC)
+template <int PPL, int SPL, int TW, bool TRACE, int G, int OCC, bool TIMED = false>
+__global__ void __launch_bounds__(SFL_GROUP_BLOCK) __attribute__((amdgpu_waves_per_eu(OCC)))
 k_wave_g(const sfl::SflMap* __restrict__ m, const sfl::SflState* __restrict__ s, const sfl::SflCtl* __restrict__ c) {
   sfl::wave::run_groups<PPL, SPL, TW, TRACE, G, TIMED>(*m, *s, *c);
 }
@@ -103,47 +98,56 @@ __global__ void __launch_bounds__(256) k_part_local(const sfl::SflMap* __restric
   const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e < s->E) sfl::env_run_part<NW>(*m, *s, *c, *P, e);
 }
-// after the wave kernel: pack each env's staged request and update records into the destination
+// after the local step: pack each env's staged request and update records into the destination
 // segments (a block reserves its range per destination with one global atomic, the envs their
-// places in it with LDS atomics), and add the envs' launch totals into P->sums.  dense: the
-// lane-per-env kernel wrote the segments itself; only the totals.
+// places in it with LDS atomics), and add the launch totals of the envs that ran into P->sums.  A
+// segment holds k_req requests / k_upd update records this round: an env with a record at or past
+// that place is deferred whole (F_DEFER; its places below it get void records, its staged records go
+// again next round and the local step skips it until then).  arrays: the lane-per-env body (its
+// scalars in the SflState / SflPart arrays), else the wave kernels' per-env blocks (eblk).
 __global__ void __launch_bounds__(256) k_part_compact(const sfl::SflPart* __restrict__ P, const sfl::SflState* __restrict__ s,
-                                                      const sfl::SflCtl* __restrict__ c, int dense) {
+                                                      const sfl::SflCtl* __restrict__ c, int arrays) {
   constexpr int MAXU = sfl::PART_UPD_ENV_MAX;  // (register arrays: the loops over them are unrolled)
   __shared__ uint32_t lreq[256], lupd[256], breq[256], bupd[256];
   __shared__ unsigned long long lsum[4][4];
-  __shared__ uint32_t lmax;
+  __shared__ uint32_t lmax, lopen, ldefer;
   const int world = P->world;
   for (int i = threadIdx.x; i < world; i += blockDim.x) lreq[i] = lupd[i] = 0u;
-  if (threadIdx.x == 0) lmax = 0u;
+  if (threadIdx.x == 0) lmax = lopen = ldefer = 0u;
   __syncthreads();
   const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
   const bool valid = e < s->E;
   int rd = -1;
-  uint32_t kr = 0, nu = 0, ku[MAXU], du[MAXU], mst = 0;
-  if (valid && !dense) {
-    rd = P->req_dst[e];
+  uint32_t kr = 0, nu = 0, ku[MAXU], du[MAXU], flags = 0;
+  // the wave kernel's per-env words (its scalar block, sfl_part.h EB_*), or the lane kernel's arrays
+  const uint32_t* eb = (valid && !arrays) ? P->eblk + (size_t)e * sfl::PART_EB : nullptr;
+  auto eb64 = [&](int i) { return (unsigned long long)eb[i] | ((unsigned long long)eb[i + 1] << 32); };
+  if (valid) {
+    flags = eb ? eb[sfl::EB_EFLAGS] : s->eflags[e];
+    rd = eb ? (int)eb[sfl::EB_REQ_DST] : P->req_dst[e];
+    nu = eb ? eb[sfl::EB_UPD_N] : P->upd_n[e];
     if (rd >= 0) kr = atomicAdd(&lreq[rd], 1u);
-    nu = P->upd_n[e];
 #pragma unroll
     for (int i = 0; i < MAXU; ++i) {
       if ((uint32_t)i < nu) {
         const sfl::PartUpd& u = P->upd_st[(size_t)e * P->upd_env + i];
         du[i] = (uint32_t)P->owner[u.port >> 2];
         ku[i] = atomicAdd(&lupd[du[i]], 1u);
-        mst = u.stage > mst ? u.stage : mst;
       }
     }
   }
-  // the envs' launch totals: wave sums, then one LDS slot per wave
-  unsigned long long a = valid ? c->launch_dec[e] : 0ull, b = valid ? c->launch_ticks[e] : 0ull,
-                     d = valid ? c->launch_bytes[e] : 0ull, o = valid ? s->err[e] : 0ull;
+  // the launch totals of the envs that ran (a deferred env sat the local step out: its totals are the
+  // last round's, already counted): wave sums, then one LDS slot per wave
+  const bool ran = valid && !(flags & sfl::F_DEFER);
+  unsigned long long a = !ran ? 0ull : eb ? eb64(sfl::EB_L_DEC) : c->launch_dec[e],
+                     b = !ran ? 0ull : eb ? eb64(sfl::EB_L_TICKS) : c->launch_ticks[e],
+                     d = !ran ? 0ull : eb ? eb64(sfl::EB_L_BYTES) : c->launch_bytes[e],
+                     o = !valid ? 0ull : eb ? eb[sfl::EB_ERR] : s->err[e];
   for (int off = 32; off > 0; off >>= 1) {
     a += __shfl_xor(a, off, 64);
     b += __shfl_xor(b, off, 64);
     d += __shfl_xor(d, off, 64);
     o |= __shfl_xor(o, off, 64);
-    mst = max(mst, (uint32_t)__shfl_xor((int)mst, off, 64));
   }
   if ((threadIdx.x & 63) == 0) {
     const int w = threadIdx.x >> 6;
@@ -151,7 +155,6 @@ __global__ void __launch_bounds__(256) k_part_compact(const sfl::SflPart* __rest
     lsum[w][1] = b;
     lsum[w][2] = d;
     lsum[w][3] = o;
-    atomicMax(&lmax, mst);
   }
   __syncthreads();
   for (int i = threadIdx.x; i < world; i += blockDim.x) {
@@ -167,18 +170,36 @@ __global__ void __launch_bounds__(256) k_part_compact(const sfl::SflPart* __rest
       atomicAdd((unsigned long long*)&P->sums[threadIdx.x], t);
     }
   }
-  if (threadIdx.x == 0 && lmax) atomicMax(P->max_stage, lmax);
   __syncthreads();  // (breq / bupd: this block's reservations)
-  // segment overflow of this round, known from the reservations: reported in this round's totals (before
-  // the last block hands them over), not in the next read
-  uint32_t ovf = 0;
-  if (valid && !dense) {
-    if (rd >= 0 && breq[rd] + kr >= P->cap_req) ovf = sfl::E_MSG_OVF;
+  // does every record of the env fit this round's segments?
+  const uint32_t kq = P->k_req, kup = P->k_upd;
+  bool fits = valid;
+  uint32_t mst = 0;
+  if (valid) {
+    if (rd >= 0 && breq[rd] + kr >= kq) fits = false;
 #pragma unroll
     for (int i = 0; i < MAXU; ++i)
-      if ((uint32_t)i < nu && bupd[du[i]] + ku[i] >= P->cap_upd) ovf = sfl::E_MSG_OVF;
+      if ((uint32_t)i < nu && bupd[du[i]] + ku[i] >= kup) fits = false;
+    if (fits)
+#pragma unroll
+      for (int i = 0; i < MAXU; ++i)
+        if ((uint32_t)i < nu) mst = max(mst, (uint32_t)P->upd_st[(size_t)e * P->upd_env + i].stage);
   }
-  if (ovf) atomicOr((unsigned long long*)&P->sums[3], (unsigned long long)ovf);
+  const bool deferred = valid && !fits;
+  const bool open = valid && (rd >= 0 || deferred);
+  const uint32_t n_open = __popcll(__ballot(open)), n_def = __popcll(__ballot(deferred));
+  for (int off = 32; off > 0; off >>= 1) mst = max(mst, (uint32_t)__shfl_xor((int)mst, off, 64));
+  if ((threadIdx.x & 63) == 0) {
+    if (n_open) atomicAdd(&lopen, n_open);
+    if (n_def) atomicAdd(&ldefer, n_def);
+    if (mst) atomicMax(&lmax, mst);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (lopen) atomicAdd(P->cnt + 2 * world + 2, lopen);
+    if (ldefer) atomicAdd(P->cnt + 2 * world + 3, ldefer);
+    if (lmax) atomicMax(P->max_stage, lmax);
+  }
   // the last block to get here writes the segment headers and hands the counts and totals to the
   // host copy (zeroing them for the next round): every block's reservations are done by then
   __shared__ bool last;
@@ -191,36 +212,100 @@ __global__ void __launch_bounds__(256) k_part_compact(const sfl::SflPart* __rest
     const uint32_t top = atomicExch(P->max_stage, 0u);
     for (int i = threadIdx.x; i < world; i += blockDim.x) {
       const uint32_t nr = atomicExch(P->cnt + i, 0u), nw = atomicExch(P->cnt + world + i, 0u);
-      P->req_out[(size_t)i * (P->cap_req + 1)].genv = nr < P->cap_req ? nr : P->cap_req;
-      sfl::PartUpd& hu = P->upd_out[(size_t)i * (P->cap_upd + 1)];
-      hu.genv = nw < P->cap_upd ? nw : P->cap_upd;
+      P->req_out[(size_t)i * (kq + 1)].genv = nr < kq ? nr : kq;
+      sfl::PartUpd& hu = P->upd_out[(size_t)i * (kup + 1)];
+      hu.genv = nw < kup ? nw : kup;
       hu.state = top;
-      co[i] = nr;
-      co[world + i] = nw;
+      co[sfl::PART_C_REQ(world) + i] = nr;
+      co[sfl::PART_C_UPD(world) + i] = nw;
+      co[sfl::PART_C_PEAK_REQ(world) + i] = max(co[sfl::PART_C_PEAK_REQ(world) + i], nr);
+      co[sfl::PART_C_PEAK_UPD(world) + i] = max(co[sfl::PART_C_PEAK_UPD(world) + i], nw);
     }
     if (threadIdx.x == 0) {
-      co[2 * world] = top;
+      const uint32_t no = atomicExch(P->cnt + 2 * world + 2, 0u), nd = atomicExch(P->cnt + 2 * world + 3, 0u);
+      co[sfl::PART_C_STAGE(world)] = top;
+      co[sfl::PART_C_OPEN(world)] = no;
+      co[sfl::PART_C_DEFER(world)] = nd;
+      co[sfl::PART_C_DEFER_SUM(world)] += nd;
       for (int i = 0; i < 3; ++i) P->cnt_out[i] += atomicExch((unsigned long long*)&P->sums[i], 0ull);
       P->cnt_out[3] |= atomicExch((unsigned long long*)&P->sums[3], 0ull);
       atomicExch(P->blocks_done, 0u);
     }
   }
-  if (!valid || dense) return;
-  if (rd >= 0) {
-    const uint32_t k = breq[rd] + kr;
-    if (k < P->cap_req) {
-      P->req_out[(size_t)rd * (P->cap_req + 1) + 1 + k] = P->req_st[e];
-      P->req_ix[e] = ((uint32_t)rd << 24) | (1u + k);
+  if (!valid) return;
+  if (fits) {
+    if (rd >= 0) {
+      const uint32_t k = breq[rd] + kr;
+      P->req_out[(size_t)rd * (kq + 1) + 1 + k] = P->req_st[e];
+      P->req_ix[e] = (uint32_t)rd * (kq + 1) + 1u + k;  // (where its reply lands: the reply segments match)
     }
-  }
 #pragma unroll
-  for (int i = 0; i < MAXU; ++i) {
-    if ((uint32_t)i < nu) {
-      const uint32_t k = bupd[du[i]] + ku[i];
-      if (k < P->cap_upd) P->upd_out[(size_t)du[i] * (P->cap_upd + 1) + 1 + k] = P->upd_st[(size_t)e * P->upd_env + i];
+    for (int i = 0; i < MAXU; ++i) {
+      if ((uint32_t)i < nu) P->upd_out[(size_t)du[i] * (kup + 1) + 1 + bupd[du[i]] + ku[i]] = P->upd_st[(size_t)e * P->upd_env + i];
+    }
+  } else {  // void records in the places below the segments' ends
+    if (rd >= 0 && breq[rd] + kr < kq) {
+      sfl::PartReq& r = P->req_out[(size_t)rd * (kq + 1) + 1 + breq[rd] + kr];
+      r.genv = 0u;
+      r.flags = sfl::REQ_VOID;
+    }
+#pragma unroll
+    for (int i = 0; i < MAXU; ++i) {
+      if ((uint32_t)i < nu && bupd[du[i]] + ku[i] < kup) {
+        sfl::PartUpd& u = P->upd_out[(size_t)du[i] * (kup + 1) + 1 + bupd[du[i]] + ku[i]];
+        u.genv = 0u;
+        u.stage = 0;
+        u.kind = sfl::UPD_VOID;
+      }
     }
   }
-  if (ovf) s->err[e] |= ovf;
+  if ((bool)(flags & sfl::F_DEFER) != deferred) {
+    if (eb) P->eblk[(size_t)e * sfl::PART_EB + sfl::EB_EFLAGS] = flags ^ sfl::F_DEFER;
+    else s->eflags[e] = flags ^ sfl::F_DEFER;
+  }
+}
+// the wave kernels' per-env scalar blocks (sfl_part.h EB_*) from the SflState arrays (dir 0: before the rounds)
+// or back into them (dir 1: before the host reads them); one thread per env
+__global__ void __launch_bounds__(256) k_part_eblk(const sfl::SflState s, uint32_t* eblk, int64_t* dec_done, int dir) {
+  const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= s.E) return;
+  uint32_t* b = eblk + (size_t)e * sfl::PART_EB;
+  const size_t E = s.E;
+  auto w32 = [&](int i, auto* a) {
+    if (dir == 0) b[i] = (uint32_t)a[e];
+    else a[e] = (std::remove_pointer_t<decltype(a)>)b[i];
+  };
+  auto w64 = [&](int i, auto* a, size_t at) {
+    uint64_t x;
+    if (dir == 0) {
+      memcpy(&x, a + at, 8);
+      b[i] = (uint32_t)x;
+      b[i + 1] = (uint32_t)(x >> 32);
+    } else {
+      x = (uint64_t)b[i] | ((uint64_t)b[i + 1] << 32);
+      memcpy(a + at, &x, 8);
+    }
+  };
+  w32(sfl::EB_PHASE, s.phase);
+  w32(sfl::EB_ELAPSED, s.elapsed);
+  w32(sfl::EB_EFLAGS, s.eflags);
+  w32(sfl::EB_EPOCH, s.epoch);
+  w32(sfl::EB_ERR, s.err);
+  w32(sfl::EB_EP_T, s.ep_t);
+  w32(sfl::EB_N_TEST, s.n_test);
+  w32(sfl::EB_N_MF, s.n_mf);
+  w32(sfl::EB_EP_DEC, s.ep_dec);
+  w32(sfl::EB_EP_TICKS, s.ep_ticks);
+  w64(sfl::EB_STEP_CTR, s.step_ctr, e);
+  w64(sfl::EB_DEC_TOTAL, s.dec_total, e);
+  w64(sfl::EB_CUM, s.cum_reward, e);
+  for (int i = 0; i < 5; ++i) w64(sfl::EB_RNG + 2 * i, s.rng, (size_t)i * E + e);
+  for (int i = 0; i < 4 * sfl::MAXW; ++i) w32(sfl::EB_MASKS + i, s.masks + (size_t)i * E);
+  w64(sfl::EB_DEC_DONE, dec_done, e);
+  if (dir == 0) {
+    b[sfl::EB_REQ_DST] = 0xFFFFFFFFu;
+    for (int i = sfl::EB_UPD_N; i < sfl::PART_EB; ++i) b[i] = 0u;
+  }
 }
 // part_answer_one (sfl_part.h) with its table reads issued together: the switch's action sources and compact
 // columns (8 bytes each), the block's width and offsets, then the row's columns, then the same comparisons in
@@ -285,14 +370,15 @@ __device__ __forceinline__ void part_answer_fast(const sfl::SflMap& m, const sfl
 __global__ void k_part_answer(const sfl::SflMap* __restrict__ m, const sfl::SflPart* __restrict__ P,
                               const sfl::PartReq* __restrict__ in, sfl::PartRep* __restrict__ out) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const size_t cap = P->cap_req;
+  const size_t cap = P->k_req;
   const size_t g = i / cap, k = i % cap + 1;
   if (g >= (size_t)P->world) return;
   const size_t base = g * (cap + 1);
+  if (k > in[base].genv || in[base + k].flags == sfl::REQ_VOID) return;
 #ifdef SFL_ANSWER_GENERIC
-  if (k <= in[base].genv) sfl::part_answer_one(*m, *P, in[base + k], out[base + k]);  // (tuning A/B)
+  sfl::part_answer_one(*m, *P, in[base + k], out[base + k]);  // (tuning A/B)
 #else
-  if (k <= in[base].genv) part_answer_fast(*m, *P, in[base + k], out[base + k]);
+  part_answer_fast(*m, *P, in[base + k], out[base + k]);
 #endif
 }
 // stage 0 (the pending updates and key-set inserts: one per env and cell) in parallel over a bounded grid
@@ -302,7 +388,7 @@ __global__ void k_part_answer(const sfl::SflMap* __restrict__ m, const sfl::SflP
 // agent-scope release fence writes its XCD's L2 back, 512 times per round; the kernel boundary does it once.)
 __global__ void __launch_bounds__(256) k_part_update(const sfl::SflMap* __restrict__ m, const sfl::SflPart* __restrict__ P,
                                                      const sfl::PartUpd* __restrict__ in) {
-  const size_t cap = P->cap_upd, stride = (size_t)gridDim.x * blockDim.x;
+  const size_t cap = P->k_upd, stride = (size_t)gridDim.x * blockDim.x;
   for (int g = 0; g < P->world; ++g) {
     const size_t base = (size_t)g * (cap + 1);
     const size_t n = in[base].genv;
@@ -447,10 +533,20 @@ struct HipBackend {
     if (d_pparams) hipFree(d_pparams);
     if (own_stream) hipStreamDestroy(own_stream);
   }
+  // the host's waits for the device (stream / event synchronisations): sfl_get_sync_count
+  uint64_t n_wait = 0;
+  hipError_t stream_wait() {
+    ++n_wait;
+    return hipStreamSynchronize(stream);
+  }
+  hipError_t event_wait(hipEvent_t ev) {
+    ++n_wait;
+    return hipEventSynchronize(ev);
+  }
   // queue on the caller's stream (e.g. torch's current stream, which its RCCL collectives follow);
   // null: back to the handle's own
   int set_stream(void* st) {
-    if (!check(hipStreamSynchronize(stream), "sync")) return -1;
+    if (!check(stream_wait(), "sync")) return -1;
     stream = st ? (hipStream_t)st : own_stream;
     return 0;
   }
@@ -465,7 +561,7 @@ struct HipBackend {
   void h2d(void* d, const void* s, size_t n) { check(hipMemcpyAsync(d, s, n, hipMemcpyHostToDevice, stream), "h2d"); }
   void d2h(void* d, const void* s, size_t n) {
     check(hipMemcpyAsync(d, s, n, hipMemcpyDeviceToHost, stream), "d2h");
-    check(hipStreamSynchronize(stream), "d2h sync");
+    check(stream_wait(), "d2h sync");
   }
   void memset(void* p, int v, size_t n) { check(hipMemsetAsync(p, v, n, stream), "memset"); }
   // stream-ordered copy without the synchronisation (the caller syncs once for several)
@@ -545,11 +641,12 @@ struct HipBackend {
   {                                                                                                             \
     constexpr sfl::WaveShape w = sfl::kVariants[v];                                                             \
     const unsigned gblocks = (unsigned)(((size_t)s.E * w.G + SFL_GROUP_BLOCK - 1) / SFL_GROUP_BLOCK);             \
-    if (c.trace) k_wave_g<w.PPL, w.SPL, w.TW, true, w.G><<<gblocks, SFL_GROUP_BLOCK, 0, stream>>>(pm, ps, pc);    \
-    else if (c.phase_cyc) k_wave_g<w.PPL, w.SPL, w.TW, false, w.G, true><<<gblocks, SFL_GROUP_BLOCK, 0, stream>>>(pm, ps, pc); \
-    else k_wave_g<w.PPL, w.SPL, w.TW, false, w.G><<<gblocks, SFL_GROUP_BLOCK, 0, stream>>>(pm, ps, pc);          \
+    if (c.trace) k_wave_g<w.PPL, w.SPL, w.TW, true, w.G, w.OCC><<<gblocks, SFL_GROUP_BLOCK, 0, stream>>>(pm, ps, pc); \
+    else if (c.phase_cyc)                                                                                       \
+      k_wave_g<w.PPL, w.SPL, w.TW, false, w.G, w.OCC, true><<<gblocks, SFL_GROUP_BLOCK, 0, stream>>>(pm, ps, pc); \
+    else k_wave_g<w.PPL, w.SPL, w.TW, false, w.G, w.OCC><<<gblocks, SFL_GROUP_BLOCK, 0, stream>>>(pm, ps, pc);   \
   }
-    static_assert(sfl::kVariants[5].TW > 64 && sfl::kNumVariants == 10, "variant 5 is the two-slot shape, 6-9 grouped");
+    static_assert(sfl::kVariants[5].TW > 64 && sfl::kNumVariants == 11, "variant 5 is the two-slot shape, 6-10 grouped");
     if (variant == 1) SFL_KW(1)
     else if (variant == 2) SFL_KW(2)
     else if (variant == 3) SFL_KW(3)
@@ -559,6 +656,7 @@ struct HipBackend {
     else if (variant == 7) SFL_KG(7)
     else if (variant == 8) SFL_KG(8)
     else if (variant == 9) SFL_KG(9)
+    else if (variant == 10) SFL_KG(10)
 #undef SFL_KG
 #undef SFL_KW2
 #undef SFL_KW
@@ -567,7 +665,7 @@ struct HipBackend {
     else k_run<4><<<blocks, 256, 0, stream>>>(pm, ps, pc);
     if (!check(hipGetLastError(), "k_run launch")) return -1;
     check(hipEventRecord(ev1, stream), "event");
-    if (!check(hipEventSynchronize(ev1), "k_run")) return -1;
+    if (!check(event_wait(ev1), "k_run")) return -1;
     float t = 0.f;
     hipEventElapsedTime(&t, ev0, ev1);
     *ms = t;
@@ -601,13 +699,13 @@ struct HipBackend {
     else k_run_ext<4><<<blocks, 64, 0, stream>>>(pm, ps, pc);
     if (!check(hipGetLastError(), "k_run_ext launch")) return -1;
     check(hipEventRecord(ev1, stream), "event");
-    if (!check(hipEventSynchronize(ev1), "k_run_ext")) return -1;
+    if (!check(event_wait(ev1), "k_run_ext")) return -1;
     float t = 0.f;
     hipEventElapsedTime(&t, ev0, ev1);
     *ms = t;
     return err.empty() ? 0 : -1;
   }
-  int sync() { return check(hipStreamSynchronize(stream), "sync") && err.empty() ? 0 : -1; }
+  int sync() { return check(stream_wait(), "sync") && err.empty() ? 0 : -1; }
   // process-wide, one per device, built on first use and kept for the life of the process
   const uint32_t* seedseq_table() {
     static uint32_t* tab[64] = {};
@@ -617,7 +715,7 @@ struct HipBackend {
       void* p = nullptr;
       if (hipMalloc(&p, n * 4) != hipSuccess) return nullptr;  // no table: draws fall back to compute
       k_seedseq_table<<<16384, 256, 0, stream>>>((uint32_t*)p, n);
-      if (!check(hipGetLastError(), "k_seedseq_table") || !check(hipStreamSynchronize(stream), "k_seedseq_table")) {
+      if (!check(hipGetLastError(), "k_seedseq_table") || !check(stream_wait(), "k_seedseq_table")) {
         hipFree(p);
         return nullptr;
       }
@@ -666,7 +764,7 @@ struct HipBackend {
     pp_host[which] = hp;
     pp_valid[which] = true;
     check(hipMemcpyAsync(dst, &pp_host[which], sizeof hp, hipMemcpyHostToDevice, stream), "params h2d");
-    check(hipStreamSynchronize(stream), "params sync");
+    check(stream_wait(), "params sync");
     return dst;
   }
   int part_local(const sfl::SflMap& m, const sfl::SflState& s, const sfl::SflCtl& c, const sfl::SflPart& P, int variant,
@@ -697,7 +795,7 @@ struct HipBackend {
     // it and syncs once; *ms is read with elapsed_ms() after that)
     *ms = 0.f;
 #ifdef SFL_PROFILE
-    if (!check(hipEventSynchronize(ev1), "k_part_local")) return -1;
+    if (!check(event_wait(ev1), "k_part_local")) return -1;
     if (variant > 0) print_prof();
 #endif
     return err.empty() ? 0 : -1;
@@ -707,9 +805,14 @@ struct HipBackend {
     sfl::SflCtl c{};
     PartParams* pp = part_params(1, m, s, c, P);
     if (!pp) return;
-    const size_t n = (size_t)P.world * P.cap_req;
+    const size_t n = (size_t)P.world * P.k_req;
     k_part_answer<<<(unsigned)((n + 63) / 64), 64, 0, stream>>>(&pp->m, &pp->P, in, out);
     check(hipGetLastError(), "k_part_answer");
+  }
+  // the wave kernels' per-env scalar blocks from / into the SflState arrays (k_part_eblk)
+  void part_eblk(const sfl::SflState& s, const sfl::SflPart& P, int dir) {
+    k_part_eblk<<<(s.E + 255) / 256, 256, 0, stream>>>(s, P.eblk, P.dec_done, dir);
+    check(hipGetLastError(), "k_part_eblk");
   }
   // every stage of the received update records, without the host knowing the highest stage
   void part_update_all(const sfl::SflMap& m, const sfl::SflPart& P, const sfl::PartUpd* in) {
@@ -717,7 +820,7 @@ struct HipBackend {
     sfl::SflCtl c{};
     PartParams* pp = part_params(2, m, s, c, P);
     if (!pp) return;
-    const size_t n = (size_t)P.world * P.cap_upd;
+    const size_t n = (size_t)P.world * P.k_upd;
     const unsigned blocks = (unsigned)std::min<size_t>((n + 255) / 256, 512);
     k_part_update<<<blocks, 256, 0, stream>>>(&pp->m, &pp->P, in);
     check(hipGetLastError(), "k_part_update");

@@ -54,6 +54,7 @@ struct SflMap {
   int32_t H, W, S, T, K, NP, HW, cell_bits;  // cell_bits: bits of a cell index (HW - 1)
   int32_t max_episode_steps, mf_min, mf_max, ntab;
   int32_t delay_thr;  // StandardObserver.delay_threshold (observer.py:221)
+  float eps_l2a, eps_l2b;  // log2(epsilon), log2(epsilon_decay_rate) in single precision (sfl_wave.h's epsilon test)
   double mf_rate, gamma, eps0, eps_decay, lr0, lr_decay, default_q;
   int64_t max_steps;
   uint64_t q_per_env;
@@ -93,6 +94,8 @@ struct SflMap {
                               // neighbour port of ports 0-3 (16 b each) in words 8-9; 10-15 spare
   const uint32_t* port_pack;  // [NP][4]: nb | len<<16; unique | q_w<<16; row_base; q_off
   const uint32_t* move_tab;   // [H*W][4 dir][4 action&3]: check_action result (see move_pack)
+  const uint32_t* move2c_tab; // [H*W][4 dir][4 action&3][4 rail action t]: move_tab's word of rail action t at the
+                              // destination of (cell, dir, action); off the grid: that destination (cell -1)
   const int32_t* tr_pack;     // [T][8]: ed, la, k, target, init_cell, init_dist, init_delay, init_dir | init_port<<16
   const uint32_t* seedseq32;  // [2^31] first 32-bit output of Generator(PCG64(SeedSequence(v))), or null
   const uint32_t* port_tr;    // [NP][4]: transition recipe of an out port o: nb(o) | unique(nb(o)) << 16;

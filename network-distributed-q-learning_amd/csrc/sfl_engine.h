@@ -9,6 +9,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <string>
 #include <vector>
 
@@ -42,7 +43,12 @@ struct Handle {
   uint64_t* d_sums = nullptr;  // [4]
   bool ext_stream = false;     // the caller's stream (sfl_set_stream): owner steps queue without a sync
   bool part_pending = false;              // a part_local's counts not read yet
+  bool part_consumed = true;              // part_counts handed out by sfl_part_counts (the next read restarts the peaks)
+  uint64_t part_reads = 0;                // host reads of the round counts (part_read): sfl_get_sync_count
   std::vector<uint32_t> part_counts;      // of the last part_local: [2 * world + 1]
+  // the partitioned wave kernels' per-env scalar blocks (SflPart::eblk): which copy is current --
+  // 0 the SflState arrays (the next part_local copies them in), 1 the blocks, 2 both
+  int eblk_state = 0;
   uint64_t* d_launch_dec = nullptr;
   uint64_t* d_launch_ticks = nullptr;
   uint64_t* d_launch_bytes = nullptr;
@@ -95,13 +101,22 @@ struct Handle {
 // One-env-per-wavefront kernel shapes (sfl_wave.h): PPL semaphore and SPL counter registers
 // per lane (ports <= 64*PPL, switches <= 64*SPL).  Index 0 = the lane-per-env kernel (k_run).
 // TW: trains per env the variant's LDS prefetch records are sized for (T <= TW).
-// G: lanes per env (64: one env per wavefront; 32 / 16: two / four envs per wavefront, run_groups).
+// G: lanes per env (64: one env per wavefront; 32 / 16 / 8: two / four / eight envs per wavefront, run_groups).
+// OCC: waves per SIMD a grouped shape's registers are budgeted for (sfl.hip k_wave_g; 0: the G = 64 kernels' own).
+#ifndef SFL_G8_OCC1
+// G = 8, one train slot per lane (maps with <= 8 trains, c2: 32 envs per 256-thread block).  Round 4: c2 at 65,536
+// envs 1,326 M agent-env-steps/s vs 853 M at G = 16 (profiles/r04c_c2_65536_g8.json, r04b_c2_65536_g16.json); a
+// G = 8 shape with four train slots per lane for c3 spilled 100 registers at 256 VGPRs: 745 M vs 1,471 M at G = 16
+// (profiles/r04c_c3_65536_g8.json), not kept
+#define SFL_G8_OCC1 4
+#endif
 struct WaveShape {
-  int PPL, SPL, TW, G;
+  int PPL, SPL, TW, G, OCC;
 };
-constexpr WaveShape kVariants[] = {{0, 0, 0, 64},   {1, 1, 32, 64},  {4, 1, 32, 64}, {4, 1, 64, 64}, {8, 2, 64, 64},
-                                   {16, 4, 128, 64}, {4, 1, 16, 16},  {16, 4, 32, 16}, {2, 1, 32, 32}, {8, 2, 32, 32}};
-constexpr int kNumVariants = 10;
+constexpr WaveShape kVariants[] = {{0, 0, 0, 64, 0},    {1, 1, 32, 64, 0},  {4, 1, 32, 64, 0}, {4, 1, 64, 64, 0},
+                                   {8, 2, 64, 64, 0},   {16, 4, 128, 64, 0}, {4, 1, 16, 16, 4}, {16, 4, 32, 16, 4},
+                                   {2, 1, 32, 32, 4},   {8, 2, 32, 32, 4},   {8, 2, 8, 8, SFL_G8_OCC1}};
+constexpr int kNumVariants = 11;
 #ifndef SFL_DEFAULT_G
 #define SFL_DEFAULT_G 16  // lane group size chosen where a grouped shape fits (SFL_WAVE_G overrides)
 #endif
@@ -113,7 +128,8 @@ constexpr int kNumVariants = 10;
 // A batch too small to fill the device at the default group size (fewer than kFillWaves wavefronts: 4 per SIMD
 // of MI355X's 1,024) takes two envs per wavefront instead of four: c2 at its stated 4,096 envs 316 M vs 276 M
 // agent-env-steps/s (G = 64: 313 M), while c3 at 16,384 envs -- 4,096 wavefronts at G = 16 -- keeps G = 16
-// (1,275 M vs 982 M at G = 64; profiles/r03d_group_size_*.json).
+// (1,275 M vs 982 M at G = 64; profiles/r03d_group_size_*.json).  Round 4, c2 at 4,096 envs: G = 8 229 M, 16 291 M,
+// 32 326 M, 64 323 M (profiles/r04c_c2_4096_g*.json).
 constexpr uint64_t kFillWaves = 4096;
 inline int choose_variant(const sfl_map_desc* md, bool backend_has_wave, std::string* why = nullptr, uint64_t n_envs = 0) {
   if (!backend_has_wave) return 0;
@@ -140,7 +156,8 @@ inline int choose_variant(const sfl_map_desc* md, bool backend_has_wave, std::st
   if (md->q_per_env >= (1ull << 32)) return no("Q-table beyond 2^32 cells per env");
   if ((int64_t)md->H * md->W >= (1 << 20) - 1) return no("grid beyond 2^20 cells");
   const char* gs = getenv("SFL_WAVE_G");
-  int want_g = gs ? atoi(gs) : SFL_DEFAULT_G;
+  // one train per lane, eight envs per wavefront, for maps with <= 8 trains (round 4)
+  int want_g = gs ? atoi(gs) : (md->T <= 8 ? 8 : SFL_DEFAULT_G);
   if (!gs && n_envs > 0 && want_g < 32 && n_envs * (uint64_t)want_g / 64 < kFillWaves) want_g = 32;
   auto fits = [&](int v) {
     const WaveShape& w = kVariants[v];
@@ -201,6 +218,9 @@ int create(const sfl_map_desc* md, const sfl_hparams* hp, uint32_t n_envs, const
   m.gamma = hp->gamma;
   m.eps0 = hp->epsilon;
   m.eps_decay = hp->epsilon_decay_rate;
+  // (log2 of 0 is -inf and of a negative value NaN: the device test is then never certain and takes the table)
+  m.eps_l2a = (float)log2(hp->epsilon);
+  m.eps_l2b = (float)log2(hp->epsilon_decay_rate);
   m.lr0 = hp->lr;
   m.lr_decay = hp->lr_decay_rate;
   m.default_q = hp->default_q;
@@ -325,8 +345,16 @@ int create(const sfl_map_desc* md, const sfl_hparams* hp, uint32_t n_envs, const
     m.sw_pack = h->upload(h->keep.back().data(), h->keep.back().size());
     h->keep.push_back(std::move(pp));
     m.port_pack = h->upload(h->keep.back().data(), h->keep.back().size());
+    // two steps ahead (the batch prefetch's reward projections, sfl_wave.h prefetch_slot)
+    std::vector<uint32_t> mv2c(HW * 64, 0u);
+    for (size_t i = 0; i < HW * 16; ++i) {
+      const int nc = (int)(mv[i] & 0xFFFFFu) - 1, nd = (int)((mv[i] >> 20) & 3u);
+      for (int n = 0; n < 4; ++n) mv2c[i * 4 + n] = nc < 0 ? ((uint32_t)nd << 20) : mv[((size_t)nc * 4 + nd) * 4 + n];
+    }
     h->keep.push_back(std::move(mv));
     m.move_tab = h->upload(h->keep.back().data(), h->keep.back().size());
+    h->keep.push_back(std::move(mv2c));
+    m.move2c_tab = h->upload(h->keep.back().data(), h->keep.back().size());
     h->keep.push_back(std::move(ptr_));
     m.port_tr = h->upload(h->keep.back().data(), h->keep.back().size());
     m.seedseq32 = h->be.seedseq_table();
@@ -450,10 +478,14 @@ int set_mf_schedule(Handle<B>* h, int32_t steps, const uint8_t* table) {
   return h->be.sync() ? fail(h->be.error()) : 0;
 }
 
+template <class B>
+int part_host_access(Handle<B>* h, bool write);
+
 // rng_states: [E][5] (state hi, state lo, inc hi, inc lo, has<<32|buf) — numpy's
 // default_rng(seed).bit_generator.state, computed on the host.
 template <class B>
 int learn_begin(Handle<B>* h, const uint64_t* rng_states) {
+  if (int rc = part_host_access(h, true)) return rc;
   const size_t E = h->E;
   std::vector<uint64_t> soa(5 * E);
   for (size_t e = 0; e < E; ++e)
@@ -473,6 +505,7 @@ int learn_begin(Handle<B>* h, const uint64_t* rng_states) {
 
 template <class B>
 int test_begin(Handle<B>* h) {
+  if (int rc = part_host_access(h, true)) return rc;
   const size_t E = h->E;
   h->be.memset(h->st.n_test, 0, E * 4);
   std::vector<int32_t> ph(E, PH_RESET);
@@ -482,6 +515,7 @@ int test_begin(Handle<B>* h) {
 
 template <class B>
 int mark_exploit_done(Handle<B>* h) {
+  if (int rc = part_host_access(h, true)) return rc;
   const size_t E = h->E;
   std::vector<uint32_t> fl(E);
   h->be.d2h(fl.data(), h->st.eflags, E * 4);
@@ -528,9 +562,25 @@ int reduce_launch(Handle<B>* h) {
 }
 
 // the per-env error flags, when the launch totals reported any (h->last_err)
+// before the host reads (write = false) or writes (true) the per-env scalars of a partitioned handle: the
+// wave kernels' blocks copied back into the SflState arrays if they are newer; after a write the next
+// part_local copies the arrays into the blocks again
+template <class B>
+int part_host_access(Handle<B>* h, bool write) {
+  if (!h->part.world || !h->part.eblk) return 0;
+  if (h->eblk_state == 1) {
+    h->be.part_eblk(h->st, h->part, 1);
+    if (h->be.sync()) return fail(h->be.error());
+    h->eblk_state = 2;
+  }
+  if (write) h->eblk_state = 0;
+  return 0;
+}
+
 template <class B>
 int scan_errors(Handle<B>* h) {
   if (!h->last_err) return 0;
+  if (int rc = part_host_access(h, false)) return rc;
   std::vector<uint32_t> err(h->E);
   h->be.d2h(err.data(), h->st.err, h->E * 4);
   if (h->be.sync()) return fail(h->be.error());
@@ -734,7 +784,7 @@ int part_config(Handle<B>* h, int rank, int world, const int32_t* owner, uint32_
   if (h->part.world) return fail("sfl_part_config: already configured");
   if (env_base + h->E > E_tot) return fail("sfl_part_config: env range outside envs_total");
   if (cap_req < h->E) return fail("sfl_part_config: request capacity must hold one request per local env");
-  if (cap_req >= (1u << 24) || cap_upd < 1) return fail("sfl_part_config: bad capacities");
+  if (cap_upd < 1 || (uint64_t)world * (cap_req + 1ull) >= (1ull << 32)) return fail("sfl_part_config: bad capacities");
   // the wave kernel stages up to upd_env update records per env and round (E_MSG_OVF beyond); the
   // segments must hold every env's staged records
   const uint32_t upd_env = cap_upd / h->E < PART_UPD_ENV_MAX ? cap_upd / h->E : PART_UPD_ENV_MAX;
@@ -772,6 +822,8 @@ int part_config(Handle<B>* h, int rank, int world, const int32_t* owner, uint32_
   P.E_tot = E_tot;
   P.cap_req = cap_req;
   P.cap_upd = cap_upd;
+  P.k_req = cap_req;  // (full segments until sfl_part_set_caps)
+  P.k_upd = cap_upd;
   P.q_own_per_env = off;
   P.own_rows = rows;
   P.own_words = (rows + 31u) / 32u;
@@ -786,29 +838,35 @@ int part_config(Handle<B>* h, int rank, int world, const int32_t* owner, uint32_
   P.obs = h->template dalloc<Obs>(h->E);
   P.req_ix = h->template dalloc<uint32_t>(h->E);
   P.dec_done = h->template dalloc<int64_t>(h->E);
-  P.cnt = h->template dalloc<uint32_t>(2 * (size_t)world + 2);
+  P.cnt = h->template dalloc<uint32_t>(2 * (size_t)world + 4);
   P.sums = h->d_sums;
-  P.cnt_out = h->template dalloc<uint64_t>(4 + (size_t)world + 1);
+  P.cnt_out = h->template dalloc<uint64_t>(4 + ((size_t)PART_NCNT(world) + 1) / 2);
   P.upd_env = upd_env;
   P.req_st = h->template dalloc<PartReq>(h->E);
   P.req_dst = h->template dalloc<int32_t>(h->E);
   P.upd_st = h->template dalloc<PartUpd>((size_t)h->E * upd_env);
   P.upd_n = h->template dalloc<uint32_t>(h->E);
   P.late = h->template dalloc<uint32_t>(1 + (size_t)world * cap_upd);
+  P.eblk = nullptr;
   if (!P.owner || !P.q_own || !P.touched_own || !P.obs || !P.req_ix || !P.dec_done || !P.cnt || !P.cnt_out || !P.req_st ||
       !P.req_dst || !P.upd_st || !P.upd_n || !P.late)
     return fail("sfl_part_config: allocation failed (out of memory?)");
   P.max_stage = P.cnt + 2 * world;
   P.blocks_done = P.cnt + 2 * world + 1;
-  h->be.memset(P.cnt, 0, (2 * (size_t)world + 2) * 4);
+  h->be.memset(P.cnt, 0, (2 * (size_t)world + 4) * 4);
   h->be.memset(P.sums, 0, 4 * 8);
-  h->be.memset(P.cnt_out, 0, 4 * 8);
+  h->be.memset(P.cnt_out, 0, (4 + ((size_t)PART_NCNT(world) + 1) / 2) * 8);
   h->be.memset(P.late, 0, 4);
   h->be.fill_f64(P.q_own, h->map.default_q, (size_t)E_tot * off);
   h->be.memset(P.touched_own, 0, (size_t)E_tot * P.own_words * 4);
   h->be.memset(P.dec_done, 0, h->E * 8);
   // a grouped shape (G < 64) becomes its one-env-per-wavefront shape: same env-major state layout
   if (h->variant > 0 && kVariants[h->variant].G != 64) h->variant = wave64_variant(h->map.S, h->map.T);
+  if (h->variant > 0) {  // the wave kernels keep each env's scalars in a block between rounds
+    P.eblk = h->template dalloc<uint32_t>((size_t)h->E * PART_EB);
+    if (!P.eblk) return fail("sfl_part_config: allocation failed (out of memory?)");
+  }
+  h->eblk_state = 0;
   // the partitioned rounds run the body the handle was created for (h->variant: k_wave where
   // eligible, else the lane-per-env body), with that body's (switch, train) slot layout
   return h->be.sync() ? fail(h->be.error()) : 0;
@@ -895,20 +953,35 @@ int part_get_q(Handle<B>* h, uint32_t genv, double* q, uint32_t* touched) {
 template <class B>
 int part_begin(Handle<B>* h) {
   if (!h->part.world) return fail("sfl_part_begin: handle not partitioned");
+  if (int rc = part_host_access(h, true)) return rc;
   h->be.memset(h->part.dec_done, 0, h->E * 8);
   return h->be.sync() ? fail(h->be.error()) : 0;
 }
 
-// the host copy of the last part_local's record counts and of the launch totals accumulated
-// since the previous read: the round's one synchronisation
+// this round's segment sizes (records per destination, without the header): the buffers handed to the
+// next rounds hold [world][k + 1] records.  Every rank of the job must use the same values.
+template <class B>
+int part_set_caps(Handle<B>* h, uint32_t k_req, uint32_t k_upd) {
+  SflPart& P = h->part;
+  if (!P.world) return fail("sfl_part_set_caps: handle not partitioned");
+  if (k_req < 1 || k_req > P.cap_req || k_upd < 1 || k_upd > P.cap_upd)
+    return fail("sfl_part_set_caps: capacities outside [1, the configured capacity]");
+  P.k_req = k_req;
+  P.k_upd = k_upd;
+  return 0;
+}
+
+// the host copy of the last part_local's record counts, of the peaks and deferrals and of the launch
+// totals accumulated since the previous read: a checkpoint's one synchronisation
 template <class B>
 int part_read(Handle<B>* h) {
   SflPart& P = h->part;
-  std::vector<uint64_t> out(4 + (size_t)P.world + 1);
+  std::vector<uint64_t> out(4 + ((size_t)PART_NCNT(P.world) + 1) / 2);
   h->be.d2h_async(out.data(), P.cnt_out, out.size() * 8);
-  h->be.memset(P.cnt_out, 0, 4 * 8);
+  h->be.memset(P.cnt_out, 0, out.size() * 8);
   if (h->be.sync()) return fail(std::string("sfl_part_local: ") + h->be.error());
   h->part_pending = false;
+  h->part_reads++;
   h->last_kernel_ms = h->be.elapsed_ms();
   h->last_dec = out[0];
   h->last_ticks = out[1];
@@ -916,7 +989,15 @@ int part_read(Handle<B>* h) {
   h->last_err = (uint32_t)out[3];
   h->total_dec += out[0];
   const uint32_t* cnt = (const uint32_t*)(out.data() + 4);
-  h->part_counts.assign(cnt, cnt + 2 * P.world + 1);
+  const int W = P.world;
+  std::vector<uint32_t> prev;
+  if (!h->part_consumed) prev.swap(h->part_counts);  // (peaks and deferrals since sfl_part_counts: merged)
+  h->part_counts.assign(cnt, cnt + PART_NCNT(W));
+  if (prev.size() == h->part_counts.size()) {
+    for (int i = PART_C_PEAK_REQ(W); i < PART_C_OPEN(W); ++i) h->part_counts[i] = std::max(h->part_counts[i], prev[i]);
+    h->part_counts[PART_C_DEFER_SUM(W)] += prev[PART_C_DEFER_SUM(W)];
+  }
+  h->part_consumed = false;
   return scan_errors(h);
 }
 
@@ -939,13 +1020,13 @@ int part_local(Handle<B>* h, int64_t budget, const void* rep_in, void* req_out, 
   c.launch_ticks = h->d_launch_ticks;
   c.launch_bytes = h->d_launch_bytes;
   float ms = 0.f;
+  if (P.eblk && h->eblk_state == 0) h->be.part_eblk(h->st, P, 0);  // (stream-ordered before the launch)
   if (h->be.part_local(h->map, h->st, c, P, h->variant, &ms)) return fail(std::string("sfl_part_local: ") + h->be.error());
+  if (P.eblk) h->eblk_state = 1;
   h->part_pending = true;
-  if (!n_req && h->ext_stream) return 0;
+  if (!n_req) return 0;  // (sfl_part_counts reads them)
   if (int rc = part_read(h)) return rc;
-  uint64_t n = 0;
-  for (int g = 0; g < P.world; ++g) n += h->part_counts[g];
-  if (n_req) *n_req = n;
+  if (n_req) *n_req = h->part_counts[PART_C_OPEN(P.world)];
   return 0;
 }
 
@@ -995,16 +1076,18 @@ int part_set_local_rows(Handle<B>* h, const uint8_t* local) {
   return h->be.sync() ? fail(h->be.error()) : 0;
 }
 
-// this rank's record counts of the last part_local: [2 * world + 1] = requests per destination,
-// updates per destination, highest update stage
+// this rank's counts (sfl_part.h PART_C_*): of the last part_local, requests and update records staged
+// per destination and the highest update stage, then the peaks per destination and the deferrals since
+// the previous read, that round's open and deferred envs.  cap >= 2 * world + 1 (the first three only)
 template <class B>
 int part_counts(Handle<B>* h, uint32_t* out, int32_t cap) {
   if (!h->part.world) return fail("sfl_part_counts: handle not partitioned");
-  const int32_t n = 2 * h->part.world + 1;
-  if (cap < n) return fail("sfl_part_counts: buffer too small");
+  const int32_t n = PART_NCNT(h->part.world);
+  if (cap < PART_NCNT_LEGACY(h->part.world)) return fail("sfl_part_counts: buffer too small");
   if (h->part_pending)
     if (int rc = part_read(h)) return rc;
-  for (int32_t i = 0; i < n; ++i) out[i] = i < (int32_t)h->part_counts.size() ? h->part_counts[i] : 0u;
+  for (int32_t i = 0; i < n && i < cap; ++i) out[i] = i < (int32_t)h->part_counts.size() ? h->part_counts[i] : 0u;
+  h->part_consumed = true;
   return 0;
 }
 

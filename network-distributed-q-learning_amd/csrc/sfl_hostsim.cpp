@@ -68,6 +68,7 @@ struct HostBackend {
     return 0;
   }
   int sync() { return 0; }
+  uint64_t n_wait = 0;  // (nothing to wait for: the host build runs on the caller's thread)
   const uint32_t* seedseq_table() { return nullptr; }  // the host build draws every sub-generator
   void reduce_launch(const uint64_t* dec, const uint64_t* ticks, const uint64_t* bytes, const uint32_t* err, uint32_t E,
                      uint64_t* out) {
@@ -90,33 +91,102 @@ struct HostBackend {
       else if (m.T <= 64) sfl::env_run_part<2>(m, s, c, P, (uint32_t)e);
       else sfl::env_run_part<4>(m, s, c, P, (uint32_t)e);
     }
-    for (int g = 0; g < P.world; ++g) sfl::part_headers(P, g);
-    uint64_t t[4];
-    reduce_launch(c.launch_dec, c.launch_ticks, c.launch_bytes, s.err, s.E, t);
-    for (int i = 0; i < 4; ++i) P.sums[i] = t[i];
-    sfl::part_finish(P);
+    part_compact(P, s, c);
     *ms = 0.f;
     return 0;
   }
+  // k_part_compact (sfl.hip) in env order: each env's staged records into the segments (at most k_req /
+  // k_upd per destination; an env with a record past that is deferred whole, its places below the end
+  // get void records), the launch totals of the envs that ran, the headers and the checkpoint counts
+  static void part_compact(const sfl::SflPart& P, const sfl::SflState& s, const sfl::SflCtl& c) {
+    const int W = P.world;
+    const uint32_t kq = P.k_req, ku = P.k_upd;
+    std::vector<uint32_t> nr(W, 0u), nw(W, 0u);
+    uint32_t top = 0, n_open = 0, n_def = 0;
+    uint64_t t[4] = {0, 0, 0, 0};
+    for (uint32_t e = 0; e < s.E; ++e) {
+      const uint32_t flags = s.eflags[e];
+      if (!(flags & sfl::F_DEFER)) {
+        t[0] += c.launch_dec[e];
+        t[1] += c.launch_ticks[e];
+        t[2] += c.launch_bytes[e];
+      }
+      t[3] |= s.err[e];
+      const int rd = P.req_dst[e];
+      const uint32_t nu = P.upd_n[e];
+      const sfl::PartUpd* st = P.upd_st + (size_t)e * P.upd_env;
+      const uint32_t kr = rd >= 0 ? nr[rd]++ : 0u;
+      uint32_t ks[sfl::PART_UPD_ENV_MAX];
+      bool fits = rd < 0 || kr < kq;
+      for (uint32_t i = 0; i < nu; ++i) {
+        const int d = P.owner[st[i].port >> 2];
+        ks[i] = nw[d]++;
+        if (ks[i] >= ku) fits = false;
+      }
+      for (uint32_t i = 0; i < nu; ++i) {
+        sfl::PartUpd& u = P.upd_out[(size_t)P.owner[st[i].port >> 2] * (ku + 1) + 1 + ks[i]];
+        if (fits) {
+          u = st[i];
+          top = st[i].stage > top ? st[i].stage : top;
+        } else if (ks[i] < ku) {
+          u.genv = 0u;
+          u.stage = 0;
+          u.kind = sfl::UPD_VOID;
+        }
+      }
+      if (rd >= 0 && (fits || kr < kq)) {
+        sfl::PartReq& r = P.req_out[(size_t)rd * (kq + 1) + 1 + kr];
+        if (fits) {
+          r = P.req_st[e];
+          P.req_ix[e] = (uint32_t)rd * (kq + 1) + 1u + kr;
+        } else {
+          r.genv = 0u;
+          r.flags = sfl::REQ_VOID;
+        }
+      }
+      if ((bool)(flags & sfl::F_DEFER) == fits) s.eflags[e] = flags ^ sfl::F_DEFER;
+      n_open += (rd >= 0 || !fits) ? 1u : 0u;
+      n_def += fits ? 0u : 1u;
+    }
+    uint32_t* co = (uint32_t*)(P.cnt_out + 4);
+    for (int g = 0; g < W; ++g) {
+      P.req_out[(size_t)g * (kq + 1)].genv = nr[g] < kq ? nr[g] : kq;
+      sfl::PartUpd& hu = P.upd_out[(size_t)g * (ku + 1)];
+      hu.genv = nw[g] < ku ? nw[g] : ku;
+      hu.state = top;
+      co[sfl::PART_C_REQ(W) + g] = nr[g];
+      co[sfl::PART_C_UPD(W) + g] = nw[g];
+      co[sfl::PART_C_PEAK_REQ(W) + g] = std::max(co[sfl::PART_C_PEAK_REQ(W) + g], nr[g]);
+      co[sfl::PART_C_PEAK_UPD(W) + g] = std::max(co[sfl::PART_C_PEAK_UPD(W) + g], nw[g]);
+    }
+    co[sfl::PART_C_STAGE(W)] = top;
+    co[sfl::PART_C_OPEN(W)] = n_open;
+    co[sfl::PART_C_DEFER(W)] = n_def;
+    co[sfl::PART_C_DEFER_SUM(W)] += n_def;
+    for (int i = 0; i < 3; ++i) P.cnt_out[i] += t[i];
+    P.cnt_out[3] |= t[3];
+  }
   int set_stream(void*) { return 0; }  // one host thread: nothing to order
+  void part_eblk(const sfl::SflState&, const sfl::SflPart&, int) {}  // (the lane body keeps the SflState arrays)
   void part_answer(const sfl::SflMap& m, const sfl::SflPart& P, const sfl::PartReq* in, sfl::PartRep* out) {
     for (int g = 0; g < P.world; ++g) {
-      const size_t base = (size_t)g * (P.cap_req + 1);
+      const size_t base = (size_t)g * (P.k_req + 1);
       const int64_t n = in[base].genv;
 #pragma omp parallel for
-      for (int64_t k = 1; k <= n; ++k) sfl::part_answer_one(m, P, in[base + k], out[base + k]);
+      for (int64_t k = 1; k <= n; ++k)
+        if (in[base + k].flags != sfl::REQ_VOID) sfl::part_answer_one(m, P, in[base + k], out[base + k]);
     }
   }
   // stage by stage up to the highest stage in the received segment headers
   void part_update_all(const sfl::SflMap& m, const sfl::SflPart& P, const sfl::PartUpd* in) {
     uint32_t top = 0;
     for (int g = 0; g < P.world; ++g) {
-      const sfl::PartUpd& hd = in[(size_t)g * (P.cap_upd + 1)];
+      const sfl::PartUpd& hd = in[(size_t)g * (P.k_upd + 1)];
       if (hd.genv > 0 && hd.state > top) top = hd.state;
     }
     for (uint32_t stage = 0; stage <= top; ++stage)
       for (int g = 0; g < P.world; ++g) {
-        const size_t base = (size_t)g * (P.cap_upd + 1);
+        const size_t base = (size_t)g * (P.k_upd + 1);
         const int64_t n = in[base].genv;
 #pragma omp parallel for
         for (int64_t k = 1; k <= n; ++k)

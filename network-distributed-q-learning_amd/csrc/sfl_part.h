@@ -8,8 +8,13 @@
 //
 // One round = every local env makes (at most) one decision:
 //   local    (env_run_part): apply the reply of the previous round's request, continue the
-//            env (post, ticks, episode ends) up to the next decision, observe it and emit its
-//            request; post steps emit update records
+//            env (post, ticks, episode ends) up to the next decision, observe it and stage its
+//            request; post steps stage update records
+//   compact  (k_part_compact): the staged records into the destination segments, at most k_req
+//            requests and k_upd update records per segment; an env whose records do not all fit
+//            is deferred whole (F_DEFER: it sends nothing this round and sits out the next local
+//            step, its staged records go again), so the segments have a fixed size and the
+//            exchange needs no counts from the host
 //   exchange updates + requests (RCCL all-to-all; segment per destination rank)
 //   update   (part_update_one): the owner applies the updates, stage by stage
 //   answer   (part_answer_one): the owner computes max(row) and the masked argmax
@@ -21,9 +26,25 @@
 
 namespace sfl {
 
-enum : uint32_t { F_REQ = 64 };  // eflags: a request is waiting for its reply
+enum : uint32_t { F_REQ = 64 };     // eflags: a request is waiting for its reply
+enum : uint32_t { F_DEFER = 256 };  // eflags: the env's staged records did not fit this round's segments
+// a record in a segment place left by a deferred env (the owner skips it): PartReq::flags / PartUpd::kind
+constexpr uint32_t REQ_VOID = 2u, UPD_VOID = 2u;
 enum : uint32_t { E_MSG_OVF = 16 };  // a message segment overflowed (capacity too small)
 constexpr uint32_t PART_UPD_ENV_MAX = 16;  // staged update records per env and round, at most
+
+// The wave kernel's per-env scalars between rounds (SflPart::eblk, [E][PART_EB] words, env-major): one
+// coalesced load and one store per env and round instead of ~30 single-word accesses to as many [field][E]
+// arrays, each a partial cache line (round 3: 67 of 115 write requests per env and round).  The canonical
+// SflState arrays are refreshed from the block when the host reads them (part_sync) and copied into it at
+// sfl_part_begin (k_part_eblk).  Word offsets:
+enum : int {
+  EB_PHASE = 0, EB_ELAPSED = 1, EB_EFLAGS = 2, EB_EPOCH = 3, EB_ERR = 4, EB_EP_T = 5, EB_N_TEST = 6, EB_N_MF = 7,
+  EB_EP_DEC = 8, EB_EP_TICKS = 9, EB_STEP_CTR = 10 /* 2 */, EB_DEC_TOTAL = 12 /* 2 */, EB_CUM = 14 /* 2, f64 */,
+  EB_RNG = 16 /* 5 x 2 */, EB_MASKS = 26 /* 4 x MAXW */, EB_DEC_DONE = 42 /* 2 */, EB_REQ_DST = 44, EB_UPD_N = 45,
+  EB_L_DEC = 46 /* 2 */, EB_L_TICKS = 48 /* 2 */, EB_L_BYTES = 50 /* 2 */, EB_USED = 52
+};
+constexpr int PART_EB = 64;
 
 // message records; record 0 of each destination segment is a header whose first word is the
 // number of records that follow
@@ -32,7 +53,7 @@ struct PartReq {
   uint16_t port;   // 4 * switch + in-port slot (the row's block)
   uint16_t amask;  // allowed actions (get_action_mask)
   uint32_t state;  // observation state index within the block
-  uint32_t flags;  // 1: exploratory action (no argmax, no key-set insert)
+  uint32_t flags;  // 1: exploratory action (no argmax, no key-set insert); REQ_VOID: no request
 };
 struct PartRep {
   int32_t action;  // masked argmax (distr_q.py:468-490); -1 for exploratory requests
@@ -45,7 +66,7 @@ struct PartUpd {
   uint8_t j;      // compact column
   uint8_t stage;  // 0: pending update / key-set inserts; 1 + i: bonus of the i-th arrived train
   uint32_t state;
-  uint32_t kind;  // 0: q <- (1 - lr) q + lr target;  1: key-set insert only
+  uint32_t kind;  // 0: q <- (1 - lr) q + lr target;  1: key-set insert only; UPD_VOID: nothing
   double lr;
   double target;
 };
@@ -57,7 +78,9 @@ struct SflPart {
                               // (its owner is this rank; all 0: every row operation as a message)
   uint32_t env_base;  // global index of local env 0
   uint32_t E_tot;     // envs over all ranks
-  uint32_t cap_req, cap_upd;  // records per destination segment (without the header)
+  uint32_t cap_req, cap_upd;  // records per destination segment (without the header), at most
+  uint32_t k_req, k_upd;      // this round's records per destination segment (<= cap; the segments of
+                              // a buffer are k + 1 records apart): sfl_part_set_caps
   uint64_t q_own_per_env;     // doubles of owned Q per env
   uint32_t own_rows, own_words;
   const int32_t* owner;       // [S] rank owning each switch agent
@@ -66,36 +89,45 @@ struct SflPart {
   double* q_own;              // [E_tot][q_own_per_env]
   uint32_t* touched_own;      // [E_tot][own_words]
   Obs* obs;                   // [E] observation waiting for its reply
-  uint32_t* req_ix;           // [E] destination << 24 | record index of that request
+  uint32_t* req_ix;           // [E] record index of that request's reply in the reply buffer
   int64_t* dec_done;          // [E] decisions since sfl_part_begin
-  uint32_t* cnt;              // [2][world] records emitted this round (requests, updates)
-  uint32_t* max_stage;        // [1] highest update stage emitted this round
+  uint32_t* cnt;              // [2][world] records staged this round (requests, updates; sent or not),
+                              // then max_stage, blocks_done, open envs, deferred envs
+  uint32_t* max_stage;        // [1] highest update stage sent this round
   uint32_t* blocks_done;      // [1] k_part_compact's finished blocks (the last one writes the headers)
   uint64_t* sums;             // [4] this round's launch totals (decisions, ticks, bytes, error bits OR)
-  uint64_t* cnt_out;          // [4 + world + 1]: sums, then the [2 * world + 1] counts (incl. max_stage) as
-                              // u32: the one host read of a round (part_finish zeroes cnt / sums for the next)
+  uint64_t* cnt_out;          // [4 + PART_NCNT(world) / 2]: sums, then the counts as u32 (PART_C_*): what the
+                              // host reads at a checkpoint (the peaks and the deferral total since the last one)
   // the wave kernel's per-env staging of a round's messages (k_part_compact packs them into the
   // segments): no record index is taken with a contended atomic counter in the env kernel
   PartReq* req_st;            // [E] the env's request of this round
-  int32_t* req_dst;           // [E] its destination rank, -1: no request
+  int32_t* req_dst;           // [E] its destination rank, -1: no request (lane-per-env body; the wave
+                              // kernels keep it in eblk)
   PartUpd* upd_st;            // [E][upd_env] the env's update records of this round
-  uint32_t* upd_n;            // [E] how many
+  uint32_t* upd_n;            // [E] how many (lane-per-env body)
   uint32_t upd_env;           // staged update records per env and round (E_MSG_OVF beyond)
   uint32_t* late;             // [1 + world * cap_upd]: count, then the received records of stage >= 1
                               // (applied in stage order by k_part_update_late)
+  uint32_t* eblk;             // [E][PART_EB] the wave kernel's per-env scalars between rounds (null: the
+                              // lane-per-env body, which keeps the SflState arrays)
   // round buffers (set per call)
-  const PartRep* rep_in;      // [world][cap_req + 1]
-  PartReq* req_out;           // [world][cap_req + 1]
-  PartUpd* upd_out;           // [world][cap_upd + 1]
+  const PartRep* rep_in;      // [world][k_req + 1]
+  PartReq* req_out;           // [world][k_req + 1]
+  PartUpd* upd_out;           // [world][k_upd + 1]
 };
 
-SFL_FN uint32_t fetch_add_u32(uint32_t* p, uint32_t v) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  return atomicAdd(p, v);
-#else
-  return __atomic_fetch_add(p, v, __ATOMIC_RELAXED);
-#endif
-}
+// the counts a checkpoint reads (sfl_part_counts), u32 words after the four launch totals of cnt_out
+SFL_FN constexpr int PART_C_REQ(int) { return 0; }                     // [world] requests staged this round
+SFL_FN constexpr int PART_C_UPD(int w) { return w; }                   // [world] update records staged
+SFL_FN constexpr int PART_C_STAGE(int w) { return 2 * w; }             // highest update stage
+SFL_FN constexpr int PART_C_PEAK_REQ(int w) { return 2 * w + 1; }      // [world] peak of C_REQ since the read
+SFL_FN constexpr int PART_C_PEAK_UPD(int w) { return 3 * w + 1; }      // [world] peak of C_UPD since the read
+SFL_FN constexpr int PART_C_OPEN(int w) { return 4 * w + 1; }          // envs with a request or deferred
+SFL_FN constexpr int PART_C_DEFER(int w) { return 4 * w + 2; }         // envs deferred this round
+SFL_FN constexpr int PART_C_DEFER_SUM(int w) { return 4 * w + 3; }     // deferrals since the read
+SFL_FN constexpr int PART_NCNT(int w) { return 4 * w + 4; }
+SFL_FN constexpr int PART_NCNT_LEGACY(int w) { return 2 * w + 1; }   // (the round-3 count vector: its prefix)
+
 SFL_FN void fetch_or_u32(uint32_t* p, uint32_t v) {
 #if defined(__HIP_DEVICE_COMPILE__)
   atomicOr(p, v);
@@ -103,31 +135,21 @@ SFL_FN void fetch_or_u32(uint32_t* p, uint32_t v) {
   __atomic_fetch_or(p, v, __ATOMIC_RELAXED);
 #endif
 }
-SFL_FN void fetch_max_u32(uint32_t* p, uint32_t v) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  atomicMax(p, v);
-#else
-  uint32_t cur = __atomic_load_n(p, __ATOMIC_RELAXED);
-  while (cur < v && !__atomic_compare_exchange_n(p, &cur, v, true, __ATOMIC_RELAXED, __ATOMIC_RELAXED)) {
-  }
-#endif
-}
-
-// the post step's Q operations as update records to the owner of the row's switch
+// the post step's Q operations as update records to the owner of the row's switch, staged in the
+// env's update slots (k_part_compact / the host build's part_compact give them their segment places)
 template <class V>
 struct MsgQ {
   V& v;
   const SflPart& P;
-  uint32_t genv;
-  double mq;  // max of the decision's own row, from the owner's reply
+  uint32_t e, genv;
+  uint32_t& n;  // records staged so far this round
+  double mq;    // max of the decision's own row, from the owner's reply
   SFL_FN void emit(int sw, int slot, uint32_t state, int j, uint32_t kind, double lr, double target, int stage) {
-    const int dst = P.owner[sw];
-    const uint32_t k = fetch_add_u32(&P.cnt[P.world + dst], 1u);
-    if (k >= P.cap_upd) {
+    if (n >= P.upd_env || stage > 254) {  // (the record's stage field is 8 bits)
       v.err |= E_MSG_OVF;
       return;
     }
-    PartUpd& u = P.upd_out[(size_t)dst * (P.cap_upd + 1) + 1 + k];
+    PartUpd& u = P.upd_st[(size_t)e * P.upd_env + n++];
     u.genv = genv;
     u.port = (uint16_t)(4 * sw + slot);
     u.j = (uint8_t)j;
@@ -136,7 +158,6 @@ struct MsgQ {
     u.kind = kind;
     u.lr = lr;
     u.target = target;
-    if (stage > 0) fetch_max_u32(P.max_stage, (uint32_t)stage);
   }
   SFL_FN void touch(int sw, int slot, uint32_t state) { emit(sw, slot, state, 0, 1u, 0.0, 0.0, 0); }
   SFL_FN double row_max_of(const Decision&) { return mq; }
@@ -157,7 +178,7 @@ SFL_FN void part_answer_one(const SflMap& m, const SflPart& P, const PartReq& r,
   const MapView mv{m};
   out.mq = row_max(mv, sw, slot, row);
   out.pad = 0;
-  if (r.flags & 1u) {
+  if (r.flags & 1u) {  // (REQ_VOID records are skipped by the callers)
     out.action = -1;
   } else {
     const uint32_t rid = P.row_own[port] + r.state;
@@ -168,6 +189,7 @@ SFL_FN void part_answer_one(const SflMap& m, const SflPart& P, const PartReq& r,
 
 // owner side: one update record of the given stage
 SFL_FN void part_update_one(const SflMap& m, const SflPart& P, const PartUpd& u) {
+  if (u.kind == UPD_VOID) return;
   const int port = u.port;
   const uint32_t rid = P.row_own[port] + u.state;
   fetch_or_u32(&P.touched_own[(size_t)u.genv * P.own_words + (rid >> 5)], 1u << (rid & 31u));
@@ -180,12 +202,16 @@ SFL_FN void part_update_one(const SflMap& m, const SflPart& P, const PartUpd& u)
 }
 
 // local side: one env for one round (env_run of sfl_core.h, with the Q row operations sent to
-// their owners).  Stops after emitting the next decision's request, or when the env has made
-// its decisions for this part_step (c.dec_budget) or reached its episode target.
+// their owners).  Stops after staging the next decision's request, or when the env has made
+// its decisions for this part_step (c.dec_budget) or reached its episode target.  A deferred env
+// (F_DEFER: its records did not fit the last round's segments) sits the round out unchanged.
 template <int NW>
 SFL_FN void env_run_part(const SflMap& m, const SflState& s, const SflCtl& c, const SflPart& P, uint32_t e) {
+  if (s.eflags[e] & F_DEFER) return;
   using V = Env<NW>;
   V v(m, s, e);
+  uint32_t n_upd = 0;
+  P.req_dst[e] = -1;
   v.flags = s.eflags[e];
   v.now = s.elapsed[e];
   v.epoch = s.epoch[e];
@@ -232,27 +258,20 @@ SFL_FN void env_run_part(const SflMap& m, const SflState& s, const SflCtl& c, co
           if (c.dec_budget > 0 && dec >= c.dec_budget) break;
           Obs o;
           decide_observe(v, o, greedy);
-          const int dst = P.owner[o.sw];
-          const uint32_t k = fetch_add_u32(&P.cnt[dst], 1u);
-          if (k >= P.cap_req) {
-            v.err |= E_MSG_OVF;
-            break;
-          }
-          PartReq& r = P.req_out[(size_t)dst * (P.cap_req + 1) + 1 + k];
+          PartReq& r = P.req_st[e];
           r.genv = genv;
           r.port = (uint16_t)(4 * o.sw + o.slot);
           r.amask = (uint16_t)o.amask;
           r.state = o.state;
           r.flags = o.explore ? 1u : 0u;
+          P.req_dst[e] = P.owner[o.sw];
           P.obs[e] = o;
-          P.req_ix[e] = ((uint32_t)dst << 24) | (1u + k);
           v.flags |= F_REQ;
           break;  // the round ends here: the owner answers before this env goes on
         }
         v.flags &= ~F_REQ;
         const Obs o = P.obs[e];
-        const uint32_t ix = P.req_ix[e];
-        const PartRep& rp = P.rep_in[(size_t)(ix >> 24) * (P.cap_req + 1) + (ix & 0xFFFFFFu)];
+        const PartRep& rp = P.rep_in[P.req_ix[e]];
         mq_cur = rp.mq;
         decide_apply(v, o, o.explore ? o.action : rp.action, d);
         abytes += 220ull + 48ull * m.sw_np[d.sw] + 8ull * m.sw_na[d.sw];
@@ -262,7 +281,7 @@ SFL_FN void env_run_part(const SflMap& m, const SflState& s, const SflCtl& c, co
       }
       if (post_now) {
         if (!(v.flags & F_GREEDY)) {
-          MsgQ<V> q{v, P, genv, mq_cur};
+          MsgQ<V> q{v, P, e, genv, n_upd, mq_cur};
           env_post(v, d, q);
         }
         v.flags &= ~F_INFLIGHT;
@@ -315,31 +334,10 @@ SFL_FN void env_run_part(const SflMap& m, const SflState& s, const SflCtl& c, co
   s.err[e] = v.err;
   s.cum_reward[e] = cum;
   P.dec_done[e] = dec;
+  P.upd_n[e] = n_upd;
   if (c.launch_dec) c.launch_dec[e] = ndec;
   if (c.launch_ticks) c.launch_ticks[e] = ticks;
   if (c.launch_bytes) c.launch_bytes[e] = abytes;
-}
-
-// write the record counts into the segment headers (after the local kernel)
-SFL_FN void part_headers(const SflPart& P, int dst) {
-  const uint32_t nr = P.cnt[dst], nu = P.cnt[P.world + dst];
-  P.req_out[(size_t)dst * (P.cap_req + 1)].genv = nr < P.cap_req ? nr : P.cap_req;
-  P.upd_out[(size_t)dst * (P.cap_upd + 1)].genv = nu < P.cap_upd ? nu : P.cap_upd;
-  P.upd_out[(size_t)dst * (P.cap_upd + 1)].state = *P.max_stage;
-}
-
-// after every destination's header: hand the counts and launch totals to the host copy and
-// zero them for the next round (so a round needs no separate clearing step)
-// (the counts are this round's; the launch totals accumulate until the host reads them)
-SFL_FN void part_finish(const SflPart& P) {
-  uint32_t* c = (uint32_t*)(P.cnt_out + 4);
-  for (int i = 0; i < 2 * P.world + 1; ++i) {
-    c[i] = P.cnt[i];
-    P.cnt[i] = 0u;
-  }
-  for (int i = 0; i < 3; ++i) P.cnt_out[i] += P.sums[i];
-  P.cnt_out[3] |= P.sums[3];
-  for (int i = 0; i < 4; ++i) P.sums[i] = 0ull;
 }
 
 }  // namespace sfl

@@ -40,6 +40,9 @@ namespace wave {
 #ifndef SFL_TICK_HOLD
 #define SFL_TICK_HOLD 2  // run_groups: ticks wait while this many groups of the wave can still decide
 #endif
+#ifndef SFL_AB_EPS_LOG
+#define SFL_AB_EPS_LOG 1  // (A/B switch, round 4) the epsilon test in the log domain, the table only when close
+#endif
 #ifndef SFL_TICK_REMMIN
 #define SFL_TICK_REMMIN 5  // ... and one of them has fewer than this many decisions left (0: hold regardless)
 #endif
@@ -159,6 +162,11 @@ __device__ __forceinline__ uint64_t r_to64(uint32_t r) {
 // decay**n beyond the host-computed tables (rare): out of line, so the f64 pow expansion does
 // not set the register budget of the whole kernel
 __device__ __attribute__((noinline)) double pow_ool(double base, double n) { return pow(base, n); }
+// random() < eps0 * decay**n on the host table's value (pow past it): out of line, the rare case of the log-domain test
+__device__ __attribute__((noinline)) bool eps_exact_ool(const double* tab, int32_t ntab, double eps0, double decay, uint32_t n,
+                                                        double u) {
+  return u < (n < (uint32_t)ntab ? ((const SFL_AS_G double*)tab)[n] : eps0 * pow(decay, (double)n));
+}
 
 __device__ __forceinline__ int ctz64(uint64_t x) { return __builtin_ctzll(x); }
 __device__ __forceinline__ int popc64(uint64_t x) { return __builtin_popcountll(x); }
@@ -210,6 +218,27 @@ __device__ __forceinline__ int mhighest(M2 m) { return m.w[1] ? 127 - __builtin_
 __device__ __forceinline__ uint64_t mfirst(uint64_t, int n) { return n >= 64 ? ~0ull : (1ull << n) - 1ull; }
 __device__ __forceinline__ M2 mfirst(M2, int n) {
   return n >= 128 ? M2{{~0ull, ~0ull}} : n >= 64 ? M2{{~0ull, (n == 64) ? 0ull : (1ull << (n - 64)) - 1ull}} : M2{{(1ull << n) - 1ull, 0ull}};
+}
+// index of the i-th set bit (i < popcount; per lane): binary search on popcounts, branch-free
+__device__ __forceinline__ int mselect(uint32_t m, int i) {
+  int base = 0;
+#pragma unroll
+  for (int w = 16; w >= 1; w >>= 1) {
+    const int c = __builtin_popcount(m & ((1u << w) - 1u));
+    const bool up = i >= c;
+    i = up ? i - c : i;
+    m = up ? m >> w : m;
+    base = up ? base + w : base;
+  }
+  return base;
+}
+__device__ __forceinline__ int mselect(uint64_t m, int i) {
+  const int c = __builtin_popcount((uint32_t)m);
+  return i >= c ? 32 + mselect((uint32_t)(m >> 32), i - c) : mselect((uint32_t)m, i);
+}
+__device__ __forceinline__ int mselect(M2 m, int i) {
+  const int c = popc64(m.w[0]);
+  return i >= c ? 64 + mselect(m.w[1], i - c) : mselect(m.w[0], i);
 }
 // train masks: one 32-bit word for up to 32 trains, one 64-bit word for up to 64, two (M2) for up to 128
 template <int BITS>
@@ -269,7 +298,7 @@ struct PortRec {
 // records to the owners
 template <int PPL, int SPL, int TWc, bool PART = false, int G = 64>
 struct WEnv {
-  static_assert(G == 64 || G == 32 || G == 16, "lane group of 16, 32 or 64 lanes");
+  static_assert(G == 64 || G == 32 || G == 16 || G == 8, "lane group of 8, 16, 32 or 64 lanes");
   static_assert(G == 64 || !PART, "the partitioned local step runs one env per wavefront");
   const SflMap& m;
   const SflState& s;
@@ -289,6 +318,11 @@ struct WEnv {
   static constexpr bool RING = !PART && TPL > 1 && RING_N > 0 && RING_N < TWc;
   static constexpr int PF_SLOTS = PART ? 1 : (RING ? RING_N : TWc);
   __device__ __forceinline__ static int pfx(int h) { return PART ? 0 : h; }
+  // RING: record i is staged by lane i % G (register slot i / G) in one pass per G records -- the lanes
+  // stage the batch's queued trains in queue order, so a batch of up to G decisions is one set of
+  // dependent loads instead of one per train slot; otherwise train h's lane stages it (slot h / G)
+  static constexpr bool PF_BY_RANK = RING;
+  static constexpr int PFS = PF_BY_RANK ? (PF_SLOTS + G - 1) / G : TPL;
   int pf_n = 0;  // RING: decisions since the batch was staged (= the record of the next one)
   static constexpr int kG = G;
   static_assert(TPL * G <= 128, "at most 128 train slots per env");
@@ -318,8 +352,8 @@ struct WEnv {
   // update's Q cell value and the slot word in LDS, and the staged offsets in VGPRs
   double* lpf;       // [TW][PF_D]: pending cell value | slot word (as bits) | row max
   uint32_t* lpi;     // [TW][PF_WI]: int16 distances, argmaxes
-  uint32_t pf_roff[TPL];  // offset of the staged row in the env's Q block (PF_NONE: none)
-  uint32_t pf_qoff[TPL];  // offset of the staged pending cell (PF_NONE: none)
+  uint32_t pf_roff[PFS];  // offset of the staged row in the env's Q block (PF_NONE: none)
+  uint32_t pf_qoff[PFS];  // offset of the staged pending cell (PF_NONE: none)
   bool pf_ok;        // uniform: this batch has been prefetched
   uint32_t lerr;  // error bits seen by this lane (OR-reduced on store)
   // this env's blocks: Q-table, key-set bitmap, (switch, train) slots (env-major [T][S] here,
@@ -349,6 +383,10 @@ struct WEnv {
   // PART: switches whose counter changed in this launch, a bitmap of (G * SPL) / 32 words after lsem0 (cset sets
   // the bit; store() writes back only those counters)
   uint32_t* ldirty = nullptr;
+  // PART: this lane's word of the env's scalar block (SflPart::eblk; lane i holds word i), loaded by load()
+  uint32_t eb_w = 0;
+  __device__ __forceinline__ uint32_t ebw(int i) const { return rl(eb_w, i); }  // (G = 64: wave-uniform)
+  __device__ __forceinline__ uint64_t ebw64(int i) const { return (uint64_t)ebw(i) | ((uint64_t)ebw(i + 1) << 32); }
   // product phase timers (the TIMED kernels that learn() / test() run; sfl_get_phase_cycles): decide<true>
   // stamps the end of its observe and epsilon-greedy sections on a sampled wavefront (tm_on); run_groups
   // reads the stamps from a deciding lane after the (divergent) decide block
@@ -367,10 +405,9 @@ struct WEnv {
       : m(m_), s(s_), e(e_), E(s_.E), lane(wlane & (G - 1)), gbase(wlane & ~(G - 1)), P(P_), lsem(lds), lcnt(lds + G * PPL),
         lpf((double*)(lds + G * (PPL + SPL))) {
 #pragma unroll
-    for (int k = 0; k < TPL; ++k) {
-      mine[k] = lane + G * k < m_.T;
-      pf_roff[k] = pf_qoff[k] = PF_NONE;
-    }
+    for (int k = 0; k < TPL; ++k) mine[k] = lane + G * k < m_.T;
+#pragma unroll
+    for (int k = 0; k < PFS; ++k) pf_roff[k] = pf_qoff[k] = PF_NONE;
     lpi = (uint32_t*)(lpf + PF_SLOTS * PF_D);
     lrng = (uint64_t*)(lds + G * (PPL + SPL) + PF_SLOTS * PF_WORDS);
     // PART: the timetable rows are read from the map (L2-resident): a launch runs one or two
@@ -499,6 +536,30 @@ struct WEnv {
 #pragma unroll
       for (int k = 1; k < TPL; ++k) v = (h / G == k) ? x[k] : v;
       return RL(v, h & (G - 1));
+    }
+  }
+  // train h's value with h varying per lane (a ds_bpermute from lane h % G of the group per slot)
+  template <class T>
+  __device__ __forceinline__ T trl_v(const T (&x)[TPL], int h) const {
+    const int a = (gbase + (h & (G - 1))) << 2;
+    T v = (T)__builtin_amdgcn_ds_bpermute(a, (int)x[0]);
+#pragma unroll
+    for (int k = 1; k < TPL; ++k) {
+      const T w = (T)__builtin_amdgcn_ds_bpermute(a, (int)x[k]);
+      v = (h / G == k) ? w : v;
+    }
+    return v;
+  }
+  // record i of a prefetch register (lane i % G, slot i / G; i group-uniform)
+  template <class T, int N>
+  __device__ __forceinline__ T rec_of(const T (&x)[N], int i) const {
+    if constexpr (N == 1) {
+      return RL(x[0], i);
+    } else {
+      T v = x[0];
+#pragma unroll
+      for (int k = 1; k < N; ++k) v = (i / G == k) ? x[k] : v;
+      return RL(v, i & (G - 1));
     }
   }
   template <class T>
@@ -789,6 +850,33 @@ struct WEnv {
     }
     if constexpr (PART) {
       if (lane < 2 * SPL) ldirty[lane] = 0u;
+      // the env's scalars: one 64-lane load of its block (see sfl_part.h EB_*)
+      eb_w = ld(P->eblk, (size_t)e * PART_EB + (uint32_t)lane);
+      now = (int32_t)ebw(EB_ELAPSED);
+      flags = ebw(EB_EFLAGS);
+      epoch = ebw(EB_EPOCH);
+      lerr = ebw(EB_ERR);
+      auto mask = [&](int k) -> Mask {
+        if constexpr (TPL * G <= 64 || TWc <= 32) return (Mask)ebw64(EB_MASKS + k * MAXW);
+        else return M2{{ebw64(EB_MASKS + k * MAXW), ebw64(EB_MASKS + k * MAXW + 2)}};
+      };
+      q_mask = mask(0);
+      arr_mask = mask(1);
+      fl_mask = mask(2);
+      mf_mask = mask(3);
+      {  // lanes 0-4: rng word `lane` (two dwords of the block, read across lanes)
+        const int l = lane < 5 ? lane : 0;
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute((EB_RNG + 2 * l) << 2, (int)eb_w);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute((EB_RNG + 2 * l + 1) << 2, (int)eb_w);
+        if (lane < 5) lrng[lane] = (uint64_t)lo | ((uint64_t)hi << 32);
+      }
+      cum = (int64_t)__longlong_as_double((long long)ebw64(EB_CUM));
+      n_mf = (int32_t)ebw(EB_N_MF);
+      ep_dec = (int32_t)ebw(EB_EP_DEC);
+      ep_ticks = (int32_t)ebw(EB_EP_TICKS);
+      step_ctr = (int32_t)ebw(EB_STEP_CTR);
+      n_dec = 0;
+      return;
     }
     now = U(ld(s.elapsed, e));
     flags = U(ld(s.eflags, e));
@@ -814,7 +902,8 @@ struct WEnv {
     step_ctr = (int32_t)U(ld(s.step_ctr, e));
     n_dec = 0;
   }
-  __device__ __forceinline__ void store(int32_t phase) {
+  // returns the env's error bits (OR over lanes); PART writes its scalars with store_eblk
+  __device__ __forceinline__ uint32_t store(int32_t phase) {
 #pragma unroll
     for (int k = 0; k < TPL; ++k) {
       const int hk = lane + G * k;
@@ -856,6 +945,7 @@ struct WEnv {
 #pragma unroll
     for (int b = 0; b < 6; ++b)
       if (BAL((lerr >> b) & 1u)) err |= 1u << b;
+    if (PART) return err;
     if (lane == 0) {
       st(s.phase, e, phase);
       st(s.elapsed, e, now);
@@ -888,6 +978,61 @@ struct WEnv {
       st(s.ep_ticks, e, ep_ticks);
       st(s.step_ctr, e, (int64_t)step_ctr);
       st(s.dec_total, e, ld(s.dec_total, e) + (int64_t)n_dec);
+    }
+    return err;
+  }
+  // PART: the env's scalar block (sfl_part.h EB_*) after the round: staged in LDS (the lsem0 region, read by
+  // store() before), then one store instruction, lane i writing word i
+  __device__ __forceinline__ void store_eblk(int32_t phase, uint32_t err, int32_t ep_t, int32_t n_test, int64_t dec_done,
+                                             int32_t req_dst, uint32_t upd_n, uint64_t l_dec, uint64_t l_ticks,
+                                             uint64_t l_bytes) {
+    if constexpr (PART) {
+      uint32_t* sg = lsem0;
+      auto put4 = [&](int i, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {  // uniform values, written by every lane
+        u4 v;
+        v[0] = a;
+        v[1] = b;
+        v[2] = c;
+        v[3] = d;
+        *(u4*)(sg + i) = v;
+      };
+      auto lo = [](uint64_t x) { return (uint32_t)x; };
+      auto hi = [](uint64_t x) { return (uint32_t)(x >> 32); };
+      const uint64_t dtot = ebw64(EB_DEC_TOTAL) + (uint64_t)n_dec;
+      const uint64_t cumd = (uint64_t)__double_as_longlong((double)cum);
+      const uint64_t r0 = lrng[0], r1 = lrng[1], r2 = lrng[2], r3 = lrng[3], r4 = lrng[4];
+      uint64_t mw[4][2];
+      auto mwords = [&](int k, const Mask& mk) {
+        if constexpr (TPL * G <= 64 || TWc <= 32) {
+          mw[k][0] = (uint64_t)mk;
+          mw[k][1] = 0ull;
+        } else {
+          mw[k][0] = mk.w[0];
+          mw[k][1] = mk.w[1];
+        }
+      };
+      mwords(0, q_mask);
+      mwords(1, arr_mask);
+      mwords(2, fl_mask);
+      mwords(3, mf_mask);
+      static_assert(EB_PHASE == 0 && EB_EP_DEC == 8 && EB_STEP_CTR == 10 && EB_RNG == 16 && EB_MASKS == 26 &&
+                        EB_DEC_DONE == 42 && EB_USED == 52 && MAXW == 4,
+                    "block layout");
+      put4(0, (uint32_t)phase, (uint32_t)now, flags, epoch);
+      put4(4, err, (uint32_t)ep_t, (uint32_t)n_test, (uint32_t)n_mf);
+      put4(8, (uint32_t)ep_dec, (uint32_t)ep_ticks, (uint32_t)step_ctr, 0u);
+      put4(12, lo(dtot), hi(dtot), lo(cumd), hi(cumd));
+      put4(16, lo(r0), hi(r0), lo(r1), hi(r1));
+      put4(20, lo(r2), hi(r2), lo(r3), hi(r3));
+      put4(24, lo(r4), hi(r4), lo(mw[0][0]), hi(mw[0][0]));
+      put4(28, lo(mw[0][1]), hi(mw[0][1]), lo(mw[1][0]), hi(mw[1][0]));
+      put4(32, lo(mw[1][1]), hi(mw[1][1]), lo(mw[2][0]), hi(mw[2][0]));
+      put4(36, lo(mw[2][1]), hi(mw[2][1]), lo(mw[3][0]), hi(mw[3][0]));
+      put4(40, lo(mw[3][1]), hi(mw[3][1]), lo((uint64_t)dec_done), hi((uint64_t)dec_done));
+      put4(44, (uint32_t)req_dst, upd_n, lo(l_dec), hi(l_dec));
+      put4(48, lo(l_ticks), hi(l_ticks), lo(l_bytes), hi(l_bytes));
+      const uint32_t v = sg[lane < EB_USED ? lane : 0];
+      if (lane < EB_USED) st(P->eblk, (size_t)e * PART_EB + (uint32_t)lane, v);
     }
   }
 
@@ -1223,12 +1368,14 @@ struct WEnv {
     mf_mask = MF;
     SFL_LAP(14);
     // _check_active_switch (switch_env.py:427-485)
-    Move amv[TPL];
+    // (the slots' move-table loads issued together)
+    int sw_next[TPL];  // the switch at the cell the train's next rail action leads to (-1: none)
 #pragma unroll
     for (int k = 0; k < TPL; ++k) {
       const bool ok = mine_(k) && pos[k] >= 0;
       const uint32_t nxt = pl_len(plan[k]) ? pl_front(plan[k]) : A_FWD;
-      amv[k] = check_action<false>(nxt, ok ? pos[k] : 0, ok ? (int)tb_dir(bits[k]) : 0);
+      const Move mv = check_action<false>(nxt, ok ? pos[k] : 0, ok ? (int)tb_dir(bits[k]) : 0);
+      sw_next[k] = mv.cell >= 0 ? dest_sw(mv) : -1;
     }
     bool act[TPL];
 #pragma unroll
@@ -1236,9 +1383,8 @@ struct WEnv {
       act[k] = false;
       const uint32_t st4 = tb_state(bits[k]);
       if (mine_(k) && pos[k] >= 0 && st4 != S_WAITING) {
-        const Move mv = amv[k];
-        if (mv.cell >= 0) {
-          const int sw_at = dest_sw(mv);
+        {
+          const int sw_at = sw_next[k];
           if (sw_at >= 0) {
             int sw = -1;
             if (st4 == S_READY || st4 == S_MOVING) sw = sw_at;
@@ -1273,23 +1419,41 @@ struct WEnv {
   __device__ __forceinline__ void prefetch(bool greedy) {
     const Mask malf = malf_mask();
 #pragma unroll
-    for (int k = 0; k < TPL; ++k) pf_roff[k] = pf_qoff[k] = PF_NONE;
+    for (int k = 0; k < PFS; ++k) pf_roff[k] = pf_qoff[k] = PF_NONE;
+    pf_n = 0;
+    if constexpr (PF_BY_RANK) {
+      // lane i stages the i-th queued train (record i = the i-th decision of the batch); trains beyond the
+      // records wait for the next staging
+      const int nq = mpopc(q_mask);
+#pragma unroll 1
+      for (int k = 0; k < PFS; ++k) {
+        const int i = lid() + G * k;
+        const bool on = i < nq && i < PF_SLOTS;
+        const int h = mselect(q_mask, on ? i : 0);
+        const uint32_t sd = trl_v(sdec, h), npv = trl_v(nprv, h), bt = trl_v(bits, h), pl = trl_v(plan, h);
+        const int32_t ps = trl_v(pos, h);
+        uint32_t roff = PF_NONE, qoff = PF_NONE;
+        if (on) prefetch_slot(h, i, sd, npv, bt, ps, pl, malf, greedy, roff, qoff);
+#pragma unroll
+        for (int j = 0; j < PFS; ++j) {
+          pf_roff[j] = j == k ? roff : pf_roff[j];
+          pf_qoff[j] = j == k ? qoff : pf_qoff[j];
+        }
+      }
+      return;
+    }
     // one train slot at a time (not unrolled): the slots' loads would otherwise be interleaved and
     // hold twice the registers; the slot's registers are selected by value, not indexed
     // PART: a launch decides one train per env (the round ends at the next request, and the staging
     // does not survive the launch): stage that train only
     const int h_first = PART ? mctz(q_mask) : -1;
-    pf_n = 0;
 #pragma unroll 1
     for (int k = 0; k < TPL; ++k) {
       if (!mbit(q_mask, lid() + G * k)) continue;
       if (PART && lid() + G * k != h_first) continue;
-      if constexpr (RING) {  // a train beyond the records waits for the next staging
-        if (mpopc(q_mask & mbelow(Mask{}, lid() + G * k)) >= PF_SLOTS) continue;
-      }
       uint32_t roff, qoff;
-      prefetch_slot(lid() + G * k, pick(sdec, k), pick(nprv, k), pick(bits, k), pick(pos, k), pick(plan, k), malf, greedy,
-                    roff, qoff);
+      prefetch_slot(lid() + G * k, pfx(lid() + G * k), pick(sdec, k), pick(nprv, k), pick(bits, k), pick(pos, k),
+                    pick(plan, k), malf, greedy, roff, qoff);
 #pragma unroll
       for (int j = 0; j < TPL; ++j) {
         pf_roff[j] = j == k ? roff : pf_roff[j];
@@ -1306,7 +1470,7 @@ struct WEnv {
   }
   // train hk (one of this lane's slots) is queued: stage its decision's inputs; its registers are
   // passed by value (sdec, nprv, bits, pos, plan); returns the staged row and pending-cell offsets
-  __device__ __forceinline__ void prefetch_slot(const int hk, const uint32_t sdec_k, const uint32_t nprv_k,
+  __device__ __forceinline__ void prefetch_slot(const int hk, const int rec, const uint32_t sdec_k, const uint32_t nprv_k,
                                                 const uint32_t bits_k, const int32_t pos_k, const uint32_t plan_k, Mask malf,
                                                 bool greedy, uint32_t& roff_out, uint32_t& qoff_out) {
     if constexpr (xp::kNoPrefetch) {
@@ -1320,8 +1484,6 @@ struct WEnv {
     const int slot = pin & 3;
     const int dir0 = (int)tb_dir(bits_k);
     const int pos0 = pos_k >= 0 ? pos_k : 0;
-    int rec = pfx(hk);
-    if constexpr (RING) rec = mpopc(q_mask & mbelow(Mask{}, hk));
     double* pfl = lpf + PF_D * rec;
     uint32_t* pfi = lpi + PF_WI * rec;
     // level 1: slot word, switch record, timetable row, the row block's port record, first moves
@@ -1345,37 +1507,45 @@ struct WEnv {
     const int32_t dd = dist_v(k, pos_k, dir0);
     int32_t d_stop, d_rt[4];
     {
+      // Both projections in one dependent level: the plan's first two moving entries (STOP entries are
+      // skipped) from the move-table row at the cell and the two-step row move2c_tab[cell, dir, a] (a: the
+      // route plan's first action, which is also the STOP plan's first move unless the plan starts with
+      // STOP -- then the route plan moves by the final action only, row0).  A STOP plan with more than two
+      // moves (rare) walks the rest with dependent loads.
+      const uint32_t body = plan_k >> 4;  // entries, 4 bits each
+      const uint32_t used = 0x1111111u & ((1u << (4u * (n_plan < 7u ? n_plan : 7u))) - 1u);
+      uint32_t isstop = ~(body ^ 0x4444444u);  // bit 0 of a nibble: the entry is STOP (A_STOP = 4)
+      isstop &= isstop >> 1;
+      isstop &= isstop >> 2;
+      const uint32_t mvb = used & ~isstop;
+      const int nmv = __builtin_popcount(mvb);
+      const uint32_t i0 = (uint32_t)__builtin_ctz(mvb | 0x10000000u);
+      const uint32_t mvb1 = mvb & (mvb - 1u);
+      const uint32_t i1 = (uint32_t)__builtin_ctz(mvb1 | 0x10000000u);
+      const uint32_t x0 = (body >> i0) & 15u, x1 = (body >> i1) & 15u;
+      const uint32_t at2 = a1 != A_STOP ? a1 : x0;
+      const u4 t2 = ld((const u4*)m.move2c_tab, (size_t)(((uint32_t)pos0 * 4u + (uint32_t)dir0) * 4u + (at2 & 3u)));
+      const bool on = pos_k >= 0;
+      // the STOP plan's walk
       int pc = pos_k, pd = dir0;
-      for (uint32_t i = 0; i < n_plan; ++i) {
-        const uint32_t a = pl_at(plan_k, i);
-        if (i == 0 && a != A_STOP && pc >= 0) {
-          const Move mv = mv_in(row0, a);
-          pc = mv.cell;
-          pd = mv.dir;
-        } else {
-          project(a, pc, pd);
+      if (on && nmv == 1) {
+        const Move mv = mv_in(row0, x0);
+        pc = mv.cell;
+        pd = mv.dir;
+      } else if (on && nmv >= 2) {
+        const Move mv = mv_in(t2, x1);
+        pc = mv.cell;
+        pd = mv.dir;
+        if (nmv > 2) {  // the rest of the walk (entries after the second move)
+          for (uint32_t i = (i1 >> 2) + 1u; i < n_plan; ++i) project(pl_at(plan_k, i), pc, pd);
         }
       }
       d_stop = dist_v(k, pc, pd);
-    }
-    {
-      int pc = pos_k, pd = dir0;
-      if (a1 != A_STOP && pos_k >= 0) {
-        const Move m1 = mv_in(row0, a1);
-        pc = m1.cell;
-        pd = m1.dir;
-      }
-      const u4 row1 = ld((const u4*)m.move_tab, (size_t)((uint32_t)(pc >= 0 ? pc : 0) * 4u + (uint32_t)pd));
       d_rt[0] = 0;  // final rail action 0 (DO_NOTHING) is never a route's
 #pragma unroll
       for (uint32_t t = 1; t < 4; ++t) {
-        int qc = pc, qd = pd;
-        if (pc >= 0) {
-          const Move mv = mv_in(row1, t);
-          qc = mv.cell;
-          qd = mv.dir;
-        }
-        d_rt[t] = dist_v(k, qc, qd);
+        const Move mv = mv_in(a1 != A_STOP ? t2 : row0, t);
+        d_rt[t] = dist_v(k, on ? mv.cell : -1, on ? mv.dir : dir0);
       }
     }
     // level 2: the pending update's block; the observation (LDS) and its row
@@ -1451,7 +1621,7 @@ struct WEnv {
   // a Q cell of this env was written (uniform offset): drop staged copies that contain it
   __device__ __forceinline__ void pf_written(uint32_t off) {
 #pragma unroll
-    for (int k = 0; k < TPL; ++k) {
+    for (int k = 0; k < PFS; ++k) {
       pf_qoff[k] = (pf_qoff[k] == off) ? PF_NONE : pf_qoff[k];
       pf_roff[k] = (off - pf_roff[k] < 4u) ? PF_NONE : pf_roff[k];
     }
@@ -1517,7 +1687,8 @@ struct WEnv {
 #pragma unroll
     for (int i = 0; i < 5; ++i) rng_w[i] = lrng[i];
     const uint32_t n_sw = cget(sw);
-    const uint32_t pf_roff_h = trl(pf_roff, h), pf_qoff_h = trl(pf_qoff, h);
+    const int pidx = PF_BY_RANK ? rec : h;  // the staged offsets' record
+    const uint32_t pf_roff_h = rec_of(pf_roff, pidx), pf_qoff_h = rec_of(pf_qoff, pidx);
     const int np = swr.np();
     const int na = swr.na();
     const uint32_t npv = trl(nprv, h);
@@ -1615,9 +1786,22 @@ struct WEnv {
       rng.buf = (uint32_t)rng_w[4];
       const uint32_t n = n_sw;
       // eps0 * decay**n (distr_q.py:59-68): host-computed table (a scalar load, K$-resident), pow beyond it
-      const double eps = xp::kEpsConst ? m.eps0
-                         : n < (uint32_t)m.ntab ? LDC(m.eps_tab, (size_t)n) : m.eps0 * pow_ool(m.eps_decay, (double)n);
-      explore = Ud(pcg_double(rng)) < eps;
+      const double ud = Ud(pcg_double(rng));
+      if (xp::kEpsConst) {
+        explore = ud < m.eps0;
+      } else if (!SFL_AB_EPS_LOG) {
+        explore = ud < (n < (uint32_t)m.ntab ? LDC(m.eps_tab, (size_t)n) : m.eps0 * pow_ool(m.eps_decay, (double)n));
+      } else {
+        // random() < eps0 * decay**n (distr_q.py:59-68, 314) decided in the log domain in single precision where
+        // that is certain -- log2(random()) more than 2^-10 away from log2(eps0) + n log2(decay), far beyond the
+        // f32 errors of both sides (< 1e-4 for n < 2^20) -- else on the host table's value itself (or pow past it):
+        // the same decision as the table's, without its load in the decision's chain (~1e-3 eps of draws fall
+        // back to it)
+        const float L = m.eps_l2a + (float)n * m.eps_l2b;
+        const float lu = __log2f((float)ud);
+        const bool yes = lu < L - 0x1p-10f, no = lu > L + 0x1p-10f;
+        explore = yes || (!no && eps_exact_ool(m.eps_tab, m.ntab, m.eps0, m.eps_decay, n, ud));
+      }
       if (explore && !observe_only) {
         const uint32_t sub_seed = pcg_bounded(rng, 2147483646u);
         const uint32_t nvalid = (uint32_t)__builtin_popcount(amask);
@@ -1641,7 +1825,9 @@ struct WEnv {
         const uint32_t la16 = (uint32_t)lid() & 15u;
         const bool is_pick = lid() < 16 && ((amask >> la16) & 1u) &&
                              (uint32_t)__builtin_popcount(amask & ((1u << la16) - 1u)) == pick;
-        action = ctz64(BAL(is_pick));
+        // (G = 8: lanes 0-7 hold actions 0-7; a 9-action switch's STOP, action 8, is the pick no lane makes)
+        const uint64_t pb = BAL(is_pick);
+        action = (G < 16 && pb == 0ull) ? 8 : ctz64(pb);
       }
       if (!observe_only) {  // uniform values, written by every lane
         lrng[0] = rng.shi;
@@ -1668,8 +1854,7 @@ struct WEnv {
     if (PART && !loc) {
       // the owner's reply: max over the full row, and the masked argmax (-1 for an exploratory request)
       const uint32_t ix = U(ld(P->req_ix, (size_t)e));
-      const vec_t<int32_t, 4> rw =
-          ld((const vec_t<int32_t, 4>*)(P->rep_in + (size_t)(ix >> 24) * (P->cap_req + 1) + (ix & 0xFFFFFFu)), 0);
+      const vec_t<int32_t, 4> rw = ld((const vec_t<int32_t, 4>*)(P->rep_in + ix), 0);
       best = arg = U(rw[0]);
       mx = __longlong_as_double(((long long)(uint32_t)U(rw[3]) << 32) | (long long)(uint32_t)U(rw[2]));
     } else if (row_hit) {
@@ -2114,10 +2299,13 @@ __device__ void run(const SflMap& m, const SflState& s, const SflCtl& c, const S
   PhaseTimer tm;
   if constexpr (TIMED) tm.start(c.phase_cyc != nullptr && blockIdx.x % TM_SAMPLE == 0u);
   v.load();
+  if constexpr (PART)
+    if (v.flags & F_DEFER) return;  // its records did not fit the last round's segments: it sits this one out
   if constexpr (xp::kLoadTwice) v.load();  // experiment build: the marginal cost of the state load
-  const int64_t dec_base = PART ? (int64_t)uni((uint64_t)ld(P->dec_done, e)) : 0;
-  int32_t phase = uni(ld(s.phase, e));
-  int32_t ep_t = uni(ld(s.ep_t, e)), n_test = uni(ld(s.n_test, e));
+  const int64_t dec_base = PART ? (int64_t)v.ebw64(EB_DEC_DONE) : 0;
+  int32_t phase = PART ? (int32_t)v.ebw(EB_PHASE) : uni(ld(s.phase, e));
+  int32_t ep_t = PART ? (int32_t)v.ebw(EB_EP_T) : uni(ld(s.ep_t, e));
+  int32_t n_test = PART ? (int32_t)v.ebw(EB_N_TEST) : uni(ld(s.n_test, e));
   uint32_t ticks = 0, abytes = 0;
   typename V::Dec d;
   d.sw = d.h = d.slot = d.action = d.j = d.reward = d.r_new = d.next_sw = 0;
@@ -2262,8 +2450,11 @@ __device__ void run(const SflMap& m, const SflState& s, const SflCtl& c, const S
       phase = PH_RESET;
     }
   }
-  v.store(phase);
+  const uint32_t err_out = v.store(phase);
   if constexpr (xp::kStoreTwice) v.store(phase);  // experiment build: the marginal cost of the state store
+  if constexpr (PART)
+    v.store_eblk(phase, err_out, ep_t, n_test, dec_base + (int64_t)v.n_dec, v.req_dst_v,
+                 v.n_upd < P->upd_env ? v.n_upd : P->upd_env, (uint64_t)v.n_dec, (uint64_t)ticks, (uint64_t)abytes);
   if constexpr (TIMED) tm.flush(c);
 #ifdef SFL_PROFILE
   prof[4] = (uint64_t)__builtin_amdgcn_s_memtime() - t_begin;
@@ -2273,12 +2464,7 @@ __device__ void run(const SflMap& m, const SflState& s, const SflCtl& c, const S
     for (int k = 0; k < 16; ++k) atomicAdd(&g_prof[16 + k], (unsigned long long)v.lap[k]);
   }
 #endif
-  if (lane == 0) {
-    if (PART) {
-      st(P->dec_done, e, dec_base + (int64_t)v.n_dec);
-      st(P->req_dst, e, v.req_dst_v);
-      st(P->upd_n, e, v.n_upd < P->upd_env ? v.n_upd : P->upd_env);
-    }
+  if (lane == 0 && !PART) {
     st(s.ep_t, e, ep_t);
     st(s.n_test, e, n_test);
     if (c.launch_dec) st(c.launch_dec, e, (uint64_t)v.n_dec);

@@ -671,6 +671,9 @@ def from_flatland_params(width: int, height: int, max_num_cities: int, number_of
             rows = min(r_fit, max(1, n_cities // cols))
             if rows * cols < 2:
                 rows, cols = min(r_fit, 2), 1
+            if n_cities > rows * cols:
+                warnings.warn(f"max_num_cities={n_cities}: only {rows * cols} cities fit a {size}x{size} grid",
+                              stacklevel=2)
             return generate_city_grid(rows, cols, n_agents, seed=int(seed), track_choices=tracks,
                                       rails=min(max(rails, 1), 2), size=size, malfunction=malfunction,
                                       name=f"flatland_{width}x{height}")

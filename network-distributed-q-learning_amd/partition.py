@@ -16,11 +16,12 @@ over the ranks as in the env-sharded mode.  Each round every env makes one decis
 
 Every env performs exactly the operations of the fused kernels in the same order, so the
 results are bit-identical to the single-process run (tests/test_partition.py).  Message
-buffers are [world][cap + 1] record segments whose first record carries the count.  On the GPU
-a round is queued on one stream (this batch's torch stream, handed to the library with
-sfl_set_stream) and synchronises once, in sfl_part_local, for the record counts; with N > 1
-ranks the counts (and each rank's highest update stage) go first, then each segment's filled
-prefix point to point.
+buffers are [world][k + 1] record segments whose first record carries the count; an env whose
+records do not fit a segment is deferred whole to a later round (k_part_compact), so each
+exchange is a fixed-size all-to-all.  On the GPU the rounds queue on one stream (this batch's
+torch stream, handed to the library with sfl_set_stream; RCCL collectives follow it): the host
+reads the counts only at checkpoint rounds (1, 2, 4, ..., 32, then every 32nd), where the ranks
+also agree on the next segment sizes -- no host synchronisation in the rounds between.
 """
 from __future__ import annotations
 
@@ -81,7 +82,7 @@ class PartitionedBatch:
                  rank: int = 0, world: int = 1, dist=None, lib: Optional[_lib.Lib] = None, device: int = 0,
                  owner: Optional[np.ndarray] = None, upd_per_env: int = 16, ntab: Optional[int] = None,
                  buffer_device: str = "cuda", local_rows=True, malfunction_stream: str = "counter",
-                 delay_threshold: int = 20):
+                 delay_threshold: int = 20, k_init: Optional[tuple] = None):
         import torch
         self.torch = torch
         kw = {} if ntab is None else dict(ntab=ntab)
@@ -125,7 +126,13 @@ class PartitionedBatch:
         self.on_gpu = dev.type == "cuda"
         self.rec = (rq.value, rp.value, up.value)
         self.rounds = 0
-        self._counts = (C.c_uint32 * (2 * self.world + 1))()
+        self._counts = (C.c_uint32 * (4 * self.world + 4))()   # sfl_part_counts, sfl_part.h PART_C_*
+        self.k_req, self.k_upd = self.cap_req, self.cap_upd
+        self.host_reads = 0   # checkpoint reads of the counts (the host's only look at a round's results)
+        self.checkpoints = 0
+        self.deferrals = 0    # envs deferred by a full segment, summed over rounds
+        if k_init is not None:  # (tests: start below the demand, so that envs are deferred)
+            self.set_caps(*k_init)
         # rows of this rank's own switches are decided on / updated in place (no message to itself).
         # local_rows: True (all own switches), False (every row operation as a message: the message
         # path measured on one rank) or a [S] mask of own switches (e.g. one block of a bigger job's
@@ -165,14 +172,14 @@ class PartitionedBatch:
         self.dist.all_reduce(sm)
         return int(mx[0]), int(sm[0])
 
-    def _any_rank(self, flag: int) -> int:
-        """MAX of a per-rank flag over the job (every rank gets the same answer)."""
+    def _all_max(self, vals):
+        """Element-wise MAX of per-rank integer vectors over the job (every rank gets the same answer)."""
         if self.dist is None or self.world == 1:
-            return flag
+            return list(vals)
         dev = "cuda" if (self.on_gpu and self.dist.get_backend() != "gloo") else "cpu"
-        t = self.torch.tensor([flag], dtype=self.torch.int64, device=dev)
+        t = self.torch.tensor(list(vals), dtype=self.torch.int64, device=dev)
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
-        return int(t[0])
+        return t.cpu().tolist()
 
     # ---- the reference's learn() set-up, on the partitioned tables ----------------------------
     def learn_begin(self):
@@ -181,94 +188,56 @@ class PartitionedBatch:
     def apply_qinit(self):
         self.batch.apply_qinit()
 
-    # ---- one part step: every env makes `decisions_per_env` decisions ---------------------------
-    def _exchange(self, recv, send):
-        """One rank: every segment is addressed to this rank (the receive buffers are the send buffers)."""
-        if recv is not send:
-            recv.copy_(send)
+    # ---- segment capacities ---------------------------------------------------------------------
+    # A round's buffers are [world][k + 1] records: k_req requests and k_upd update records per
+    # destination.  An env whose records do not all fit is deferred whole by k_part_compact (it
+    # sends nothing that round, sits out the next local step and sends the same records again),
+    # so results never depend on k.  At a checkpoint the ranks agree (one MAX all-reduce) on k from
+    # the peak per-destination demand since the previous checkpoint: every round in between is a
+    # fixed-size all-to-all that needs no counts from the host.  One rank keeps the full capacities
+    # (its exchange is the identity: nothing to save, nothing to defer).
+    def set_caps(self, k_req: int, k_upd: int):
+        k_req, k_upd = int(k_req), int(k_upd)
+        if (k_req, k_upd) != (self.k_req, self.k_upd):
+            self.lib.check(self.lib.dll.sfl_part_set_caps(self.batch.h, k_req, k_upd), "sfl_part_set_caps")
+            self.k_req, self.k_upd = k_req, k_upd
 
-    # ---- size-aware exchange (N > 1 ranks) ----------------------------------------------------------
-    # Each destination segment's filled prefix (header record + its records) travels as one
-    # point-to-point message into the same place of the receiver's segment: the owner kernels
-    # read a segment only up to its header count, so nothing beyond the prefix is needed.  On
-    # NCCL/RCCL the messages go device to device; gloo (the multi-rank rehearsal with GPU buffers on
-    # one box, or host buffers) stages each prefix through host memory.
-    def _sized(self) -> bool:
-        return self.dist is not None and self.world > 1
+    @staticmethod
+    def _resize(k: int, peak: int, cap: int) -> int:
+        want = min(cap, max(16, -(-(peak + peak // 4 + 16) // 16) * 16))
+        return want if (want > k or 2 * want < k) else k
 
-    def _host_staged(self) -> bool:
-        return self.on_gpu and self.dist.get_backend() == "gloo"
+    def _view(self, buf, k, rec):
+        return buf[:self.world * (k + 1) * rec]
 
-    def _p2p(self, recv, send, cap, rec, n_send, n_recv):
-        torch, dist = self.torch, self.dist
-        rs, ss = recv.view(self.world, (cap + 1) * rec), send.view(self.world, (cap + 1) * rec)
-        ops, landing = [], []
-        row = (cap + 1) * rec
-        staged = self._host_staged()
-        for p in range(self.world):
-            k_s, k_r = (int(n_send[p]) + 1) * rec, (int(n_recv[p]) + 1) * rec
-            if k_s > row or k_r > row:
-                raise _lib.SflError(f"rank {self.rank}: segment to/from rank {p} exceeds its capacity ({cap} records)")
-            if p == self.rank:
-                rs[p, :k_r].copy_(ss[p, :k_s])
-                continue
-            if staged:
-                r = torch.empty(k_r, dtype=torch.uint8)
-                landing.append((rs[p, :k_r], r))
-                ops.append(dist.P2POp(dist.isend, ss[p, :k_s].cpu(), p))
-                ops.append(dist.P2POp(dist.irecv, r, p))
-            else:
-                ops.append(dist.P2POp(dist.isend, ss[p, :k_s], p))
-                ops.append(dist.P2POp(dist.irecv, rs[p, :k_r], p))
-        if ops:
-            for r in dist.batch_isend_irecv(ops):
-                r.wait()
-        for dst, r in landing:
-            dst.copy_(r)
-
-    def _local_counts(self):
-        """(requests, update records) per destination and the highest update stage of this rank's
-        last sfl_part_local, or None if its envs reported an error (the round's synchronisation)."""
-        w = self.world
-        if self.lib.dll.sfl_part_counts(self.batch.h, self._counts, 2 * w + 1):
-            return None
-        c = list(self._counts)
-        return c[:w], c[w:2 * w], c[2 * w]
-
-    def _exchange_sized(self, err: int = 0):
-        """Updates and requests: counts first (one small all-to-all, which also carries this rank's
-        error flag and highest update stage to every rank), then the filled prefixes.  Returns the
-        job-wide error flag; on an error nothing else is exchanged (every rank stops at the same point)."""
-        torch = self.torch
-        rq, _, up = self.rec
-        counts = None if err else self._local_counts()
-        if counts is None:
-            err = 1
-            n_req, n_upd, mst = [0] * self.world, [0] * self.world, 0
+    def _a2a(self, recv, send, k, rec):
+        """Fixed-size all-to-all of the [world][k + 1]-record segments (RCCL device to device; gloo with
+        device buffers stages them through host memory)."""
+        r, s_ = self._view(recv, k, rec), self._view(send, k, rec)
+        if self.world == 1:
+            if r.data_ptr() != s_.data_ptr():
+                r.copy_(s_)
+            return
+        if self.on_gpu and self.dist.get_backend() == "gloo":
+            rc = self.torch.empty(r.numel(), dtype=self.torch.uint8)
+            self.dist.all_to_all_single(rc, s_.cpu())
+            r.copy_(rc)
         else:
-            n_req, n_upd, mst = counts
-        # row d: what this rank sends to rank d (and, in every row, its total of requests: the job's
-        # open requests end the step)
-        dev = "cpu" if self.dist.get_backend() == "gloo" else self.req_send.device
-        tot = sum(n_req)
-        cs = torch.tensor([[n_req[d], n_upd[d], int(err), mst, tot] for d in range(self.world)], dtype=torch.int64,
-                          device=dev)
-        cr = torch.empty_like(cs)
-        self.dist.all_to_all_single(cr, cs)                    # row s: what rank s sends to this rank
-        cr = cr.cpu().tolist()
-        if any(c[2] for c in cr):
-            return 1
-        self._job_open = sum(c[4] for c in cr)
-        self._n_req_sent = list(n_req)
-        self._n_req_recv = [c[0] for c in cr]
-        self._p2p(self.upd_recv, self.upd_send, self.cap_upd, up, n_upd, [c[1] for c in cr])
-        self._p2p(self.req_recv, self.req_send, self.cap_req, rq, self._n_req_sent, self._n_req_recv)
-        return 0
+            self.dist.all_to_all_single(r, s_)
 
-    def _exchange_replies_sized(self):
-        """A reply segment to rank s holds one reply per request received from s."""
-        rp = self.rec[1]
-        self._p2p(self.rep_recv, self.rep_send, self.cap_req, rp, self._n_req_recv, self._n_req_sent)
+    def _read_counts(self):
+        """This rank's counts since the previous checkpoint (sfl_part_counts: the checkpoint's host
+        synchronisation), or None if its envs reported an error."""
+        self.host_reads += 1
+        if self.lib.dll.sfl_part_counts(self.batch.h, self._counts, len(self._counts)):
+            return None
+        return list(self._counts)
+
+    def sync_count(self):
+        """(device waits, count reads) of this rank's library handle so far (sfl_get_sync_count)."""
+        w, r = C.c_uint64(), C.c_uint64()
+        self.lib.check(self.lib.dll.sfl_get_sync_count(self.batch.h, C.byref(w), C.byref(r)), "sfl_get_sync_count")
+        return w.value, r.value
 
     def step(self, decisions_per_env: int) -> int:
         """Advance every local env by ``decisions_per_env`` learning decisions (the sfl_step contract);
@@ -278,62 +247,60 @@ class PartitionedBatch:
         with self.torch.cuda.stream(self.stream):
             return self._step(decisions_per_env)
 
+    def _checkpoint(self, r: int, last: int) -> bool:
+        """Rounds after which the host reads the counts: 1, 2, 4, ..., 32, every 32nd, the round a step
+        without deferrals ends at (decisions + 1), and every 8th after it."""
+        return (r & (r - 1) == 0 and r <= 32) or r % 32 == 0 or r == last or (r > last and (r - last) % 8 == 0)
+
     def _step(self, decisions_per_env: int) -> int:
         d = self.lib.dll
         h = self.batch.h
+        W = self.world
         ptr = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
         self.lib.check(d.sfl_part_begin(h), "sfl_part_begin")
-        sized = self._sized()
-        # one rank on the GPU: the rounds queue on the stream without a synchronisation, and the counts
-        # (open requests, the envs' errors) are read only after rounds 1, 2, 4, ..., 32 and then every
-        # 32nd (with every row in place one round is the whole step; with messages the step runs its
-        # decisions + 1 rounds, the last few possibly empty).  Otherwise (N > 1 ranks, or the host
-        # build) each round's counts end the step as soon as no request is open anywhere
-        deferred = self.stream is not None and not sized
-        rounds = 0
-        n_open = 0
+        rq, rp, up = self.rec
         last = int(decisions_per_env) + 1
-        for _ in range(last):
-            n = C.c_uint64(0)
-            # a failure on one rank (error flags of its envs, message overflow) must stop every rank,
-            # or the others would wait forever in the next exchange: the flag travels with the counts
-            rc = d.sfl_part_local(h, int(decisions_per_env), ptr(self.rep_recv), ptr(self.req_send),
-                                  ptr(self.upd_send), None if (deferred or sized) else C.byref(n))
-            msg = d.sfl_last_error().decode(errors="replace") if rc else ""
-            if sized:
-                failed = self._exchange_sized(err=1 if rc else 0)
-                if failed and not msg:
-                    msg = d.sfl_last_error().decode(errors="replace")
-                n_open = self._job_open if not failed else 0
-            else:
-                failed = self._any_rank(1 if rc else 0)
-                n_open = n.value
-            if failed:
-                raise _lib.SflError(f"rank {self.rank}: sfl_part_local: " +
-                                    (msg or "stopped because another rank failed"))
-            if not sized:
-                self._exchange(self.upd_recv, self.upd_send)
-                self._exchange(self.req_recv, self.req_send)
-            self.lib.check(d.sfl_part_update(h, ptr(self.upd_recv)), "sfl_part_update")
-            self.lib.check(d.sfl_part_answer(h, ptr(self.req_recv), ptr(self.rep_send)), "sfl_part_answer")
-            if sized:
-                self._exchange_replies_sized()
-            else:
-                self._exchange(self.rep_recv, self.rep_send)
+        limit = 4 * last + 64  # (deferrals add rounds; each checkpoint resizes the segments to the demand)
+        rounds, failed, msg = 0, False, ""
+        while True:
             rounds += 1
-            if deferred and (rounds & (rounds - 1) == 0 and rounds <= 32 or rounds % 32 == 0 or rounds == last):
-                counts = self._local_counts()
-                if counts is None:
-                    raise _lib.SflError(f"rank {self.rank}: sfl_part_local: " +
-                                        d.sfl_last_error().decode(errors="replace"))
-                n_open = sum(counts[0])
-                if n_open == 0:
-                    break
-            elif not deferred and n_open == 0:
+            if not failed:
+                # a failure on this rank (a launch error) must not leave the others waiting in the next
+                # exchange: it sends empty segments until the checkpoint, where every rank stops
+                rc = d.sfl_part_local(h, int(decisions_per_env), ptr(self.rep_recv), ptr(self.req_send),
+                                      ptr(self.upd_send), None)
+                if rc:
+                    failed, msg = True, d.sfl_last_error().decode(errors="replace")
+            if failed and W > 1:
+                self._view(self.req_send, self.k_req, rq).view(W, -1)[:, :rq].zero_()
+                self._view(self.upd_send, self.k_upd, up).view(W, -1)[:, :up].zero_()
+                self._view(self.rep_send, self.k_req, rp).zero_()
+            self._a2a(self.upd_recv, self.upd_send, self.k_upd, up)
+            self._a2a(self.req_recv, self.req_send, self.k_req, rq)
+            if not failed:
+                self.lib.check(d.sfl_part_update(h, ptr(self.upd_recv)), "sfl_part_update")
+                self.lib.check(d.sfl_part_answer(h, ptr(self.req_recv), ptr(self.rep_send)), "sfl_part_answer")
+            self._a2a(self.rep_recv, self.rep_send, self.k_req, rp)
+            if not self._checkpoint(rounds, last) and rounds < limit:
+                continue
+            self.checkpoints += 1
+            c = None if failed else self._read_counts()
+            if c is None and not msg:
+                msg = d.sfl_last_error().decode(errors="replace")
+            err = 1 if c is None else 0
+            c = c or [0] * len(self._counts)
+            self.deferrals += c[4 * W + 3]
+            job = self._all_max([err, c[4 * W + 1], max(c[2 * W + 1:3 * W + 1]), max(c[3 * W + 1:4 * W + 1])])
+            if job[0]:
+                raise _lib.SflError(f"rank {self.rank}: sfl_part_local: " + (msg or "stopped because another rank failed"))
+            if job[1] == 0:
                 break  # every env has made its decisions (this round's updates are applied)
-        if (not sized) and self._any_rank(1 if n_open != 0 else 0) or sized and n_open != 0:
-            raise _lib.SflError(f"rank {self.rank}: requests still open after the last round "
-                                f"({n_open} on this rank)")
+            if rounds >= limit:
+                raise _lib.SflError(f"rank {self.rank}: requests still open after {rounds} rounds "
+                                    f"({c[4 * W + 1]} envs on this rank)")
+            if W > 1:
+                self.set_caps(self._resize(self.k_req, job[2], self.cap_req),
+                              self._resize(self.k_upd, job[3], self.cap_upd))
         self.rounds += rounds
         return rounds
 

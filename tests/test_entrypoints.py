@@ -85,8 +85,8 @@ def test_main_ini_size_keys_honour_the_grid(tmp_path):
     with pytest.warns(UserWarning, match="cities fit"):
         sc = main.build_scenario(cfg)
     assert (sc.width, sc.height) == (80, 80) and len(sc.trains) == 15
-    # max_rails_between_cities = 2: passing loops beside the backbone segments (more switches than the
-    # single-track layout of the same seed)
+    # max_rails_between_cities = 2: round 4's city grid (7 x 2 cities joined by links of their own; more switches
+    # than the single-track backbone layout of the same seed)
     mapgen = importlib.import_module("network-distributed-q-learning_amd.mapgen")
     comp = importlib.import_module("network-distributed-q-learning_amd.compiler")
     import warnings

@@ -25,18 +25,22 @@ def lib():
     return _lib.load_product()
 
 
-@pytest.fixture(params=["wave", "wave32", "scalar"])
+@pytest.fixture(params=["wave", "wave32", "wave8", "scalar"])
 def kernel(request, monkeypatch):
     """Which device kernel a Batch created inside the test runs (chosen at sfl_create):
     'wave' = k_wave at the default group size (four envs per wavefront for maps with <= 32 trains: the
     bench kernel), 'wave32' = two envs per wavefront (what a batch too small to fill the device gets,
-    sfl_engine.h choose_variant), 'scalar' = k_run."""
+    sfl_engine.h choose_variant), 'wave8' = eight envs per wavefront, one train per lane (the default for
+    maps with <= 8 trains and batches that fill the device; maps with more trains fall back to one env per
+    wavefront), 'scalar' = k_run."""
     monkeypatch.delenv("SFL_KERNEL", raising=False)
     monkeypatch.delenv("SFL_WAVE_G", raising=False)
     if request.param == "scalar":
         monkeypatch.setenv("SFL_KERNEL", "scalar")
     elif request.param == "wave":
         monkeypatch.setenv("SFL_WAVE_G", "16")
+    elif request.param == "wave8":
+        monkeypatch.setenv("SFL_WAVE_G", "8")
     else:
         monkeypatch.setenv("SFL_WAVE_G", "32")
     return request.param
@@ -205,7 +209,7 @@ def test_partitioned_rounds_gpu_equal_fused(lib, cfg, E, kernel, local_rows):
     row operation as a message (decisions + 1 rounds), or keeps only block 0 of a 4-rank partition
     in place (a 4-rank job's message traffic on one rank)."""
     import torch
-    if kernel == "wave32":
+    if kernel in ("wave32", "wave8"):
         pytest.skip("the partitioned local step runs one env per wavefront whatever the fused group size")
     part = importlib.import_module("network-distributed-q-learning_amd.partition")
     sc = _golden.load(cfg[7:])["scenario_obj"] if cfg.startswith("golden:") else mapgen.make_config(cfg)
@@ -277,6 +281,25 @@ def test_two_rank_partition_wave_gpu(lib, cfg, world):
     bit-equal to the fused run of all envs (host build)."""
     from tests import test_partition
     test_partition.two_rank_run(cfg, gpu=True, world=world)
+
+
+def test_two_rank_partition_gpu_rounds_queue_between_checkpoints(lib):
+    """Two ranks on GPU 0 over gloo, one 1,024-decision step: between checkpoint rounds the library neither
+    waits for the device nor reads a count (tests/test_partition.py _check_round_log), bit-equal to the
+    fused run.  (gloo itself stages each device segment through host memory; RCCL moves it device to
+    device on the same stream.)"""
+    from tests import test_partition
+    for st in test_partition.two_rank_run("c5", gpu=True, world=2, steps=(1024,), log_rounds=True):
+        s = st[1024]
+        assert s["rounds"] >= 1025 and s["reads"] == s["checkpoints"]
+
+
+def test_two_rank_partition_gpu_deferred_envs_bit_equal(lib):
+    """k_part_compact's deferral on the device: segments of 1 request / 2 update records per destination to
+    start with, envs deferred whole and skipped by the wave kernel's local step until they fit."""
+    from tests import test_partition
+    stats = test_partition.two_rank_run("c5", gpu=True, world=2, steps=(90, 60), k_init=(1, 2))
+    assert sum(st["deferrals"] for st in stats) > 0
 
 
 @pytest.mark.parametrize("S,T,variant", [(64, 48, 3), (100, 48, 4), (120, 64, 4), (100, 100, 5), (200, 40, 5),
