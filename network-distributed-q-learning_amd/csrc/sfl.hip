@@ -767,6 +767,22 @@ struct HipBackend {
     check(stream_wait(), "params sync");
     return dst;
   }
+  // new segment capacities (sfl_part_set_caps, at a checkpoint): the uploaded parameter blocks take them now, so
+  // the next rounds' launches find their blocks unchanged and upload nothing (no wait between checkpoints)
+  void part_caps(const sfl::SflPart& P) {
+    if (!d_pparams) return;
+    constexpr size_t stride = (sizeof(PartParams) + 255) / 256 * 256;
+    bool any = false;
+    for (int w = 0; w < 3; ++w) {
+      if (!pp_valid[w]) continue;
+      pp_host[w].P.k_req = P.k_req;
+      pp_host[w].P.k_upd = P.k_upd;
+      check(hipMemcpyAsync((char*)d_pparams + w * stride, &pp_host[w], sizeof(PartParams), hipMemcpyHostToDevice, stream),
+            "params h2d");
+      any = true;
+    }
+    if (any) check(stream_wait(), "params sync");
+  }
   int part_local(const sfl::SflMap& m, const sfl::SflState& s, const sfl::SflCtl& c, const sfl::SflPart& P, int variant,
                  float* ms) {
     PartParams* pp = part_params(0, m, s, c, P);

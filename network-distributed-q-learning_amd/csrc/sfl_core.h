@@ -54,7 +54,6 @@ struct SflMap {
   int32_t H, W, S, T, K, NP, HW, cell_bits;  // cell_bits: bits of a cell index (HW - 1)
   int32_t max_episode_steps, mf_min, mf_max, ntab;
   int32_t delay_thr;  // StandardObserver.delay_threshold (observer.py:221)
-  float eps_l2a, eps_l2b;  // log2(epsilon), log2(epsilon_decay_rate) in single precision (sfl_wave.h's epsilon test)
   double mf_rate, gamma, eps0, eps_decay, lr0, lr_decay, default_q;
   int64_t max_steps;
   uint64_t q_per_env;

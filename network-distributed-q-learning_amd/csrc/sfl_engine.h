@@ -219,8 +219,6 @@ int create(const sfl_map_desc* md, const sfl_hparams* hp, uint32_t n_envs, const
   m.eps0 = hp->epsilon;
   m.eps_decay = hp->epsilon_decay_rate;
   // (log2 of 0 is -inf and of a negative value NaN: the device test is then never certain and takes the table)
-  m.eps_l2a = (float)log2(hp->epsilon);
-  m.eps_l2b = (float)log2(hp->epsilon_decay_rate);
   m.lr0 = hp->lr;
   m.lr_decay = hp->lr_decay_rate;
   m.default_q = hp->default_q;
@@ -968,7 +966,8 @@ int part_set_caps(Handle<B>* h, uint32_t k_req, uint32_t k_upd) {
     return fail("sfl_part_set_caps: capacities outside [1, the configured capacity]");
   P.k_req = k_req;
   P.k_upd = k_upd;
-  return 0;
+  h->be.part_caps(P);
+  return h->be.error()[0] ? fail(std::string("sfl_part_set_caps: ") + h->be.error()) : 0;
 }
 
 // the host copy of the last part_local's record counts, of the peaks and deferrals and of the launch

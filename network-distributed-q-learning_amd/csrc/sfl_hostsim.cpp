@@ -167,7 +167,8 @@ struct HostBackend {
     P.cnt_out[3] |= t[3];
   }
   int set_stream(void*) { return 0; }  // one host thread: nothing to order
-  void part_eblk(const sfl::SflState&, const sfl::SflPart&, int) {}  // (the lane body keeps the SflState arrays)
+  void part_eblk(const sfl::SflState&, const sfl::SflPart&, int) {}
+  void part_caps(const sfl::SflPart&) {}  // (the host build reads the SflPart itself)  // (the lane body keeps the SflState arrays)
   void part_answer(const sfl::SflMap& m, const sfl::SflPart& P, const sfl::PartReq* in, sfl::PartRep* out) {
     for (int g = 0; g < P.world; ++g) {
       const size_t base = (size_t)g * (P.k_req + 1);

@@ -40,9 +40,6 @@ namespace wave {
 #ifndef SFL_TICK_HOLD
 #define SFL_TICK_HOLD 2  // run_groups: ticks wait while this many groups of the wave can still decide
 #endif
-#ifndef SFL_AB_EPS_LOG
-#define SFL_AB_EPS_LOG 1  // (A/B switch, round 4) the epsilon test in the log domain, the table only when close
-#endif
 #ifndef SFL_TICK_REMMIN
 #define SFL_TICK_REMMIN 5  // ... and one of them has fewer than this many decisions left (0: hold regardless)
 #endif
@@ -162,11 +159,6 @@ __device__ __forceinline__ uint64_t r_to64(uint32_t r) {
 // decay**n beyond the host-computed tables (rare): out of line, so the f64 pow expansion does
 // not set the register budget of the whole kernel
 __device__ __attribute__((noinline)) double pow_ool(double base, double n) { return pow(base, n); }
-// random() < eps0 * decay**n on the host table's value (pow past it): out of line, the rare case of the log-domain test
-__device__ __attribute__((noinline)) bool eps_exact_ool(const double* tab, int32_t ntab, double eps0, double decay, uint32_t n,
-                                                        double u) {
-  return u < (n < (uint32_t)ntab ? ((const SFL_AS_G double*)tab)[n] : eps0 * pow(decay, (double)n));
-}
 
 __device__ __forceinline__ int ctz64(uint64_t x) { return __builtin_ctzll(x); }
 __device__ __forceinline__ int popc64(uint64_t x) { return __builtin_popcountll(x); }
@@ -385,6 +377,9 @@ struct WEnv {
   uint32_t* ldirty = nullptr;
   // PART: this lane's word of the env's scalar block (SflPart::eblk; lane i holds word i), loaded by load()
   uint32_t eb_w = 0;
+  // PART: the reply to the env's last request (action, max lo / hi words), loaded by load() right behind the
+  // state (its place, req_ix, with the state batch): the apply pass reads registers instead of two dependent loads
+  uint32_t rep_a = 0, rep_lo = 0, rep_hi = 0;
   __device__ __forceinline__ uint32_t ebw(int i) const { return rl(eb_w, i); }  // (G = 64: wave-uniform)
   __device__ __forceinline__ uint64_t ebw64(int i) const { return (uint64_t)ebw(i) | ((uint64_t)ebw(i + 1) << 32); }
   // product phase timers (the TIMED kernels that learn() / test() run; sfl_get_phase_cycles): decide<true>
@@ -797,6 +792,11 @@ struct WEnv {
     // loads each sat in its own exec-masked block and waited for its own HBM round trip (16 + 4 + 2 x 8 in a
     // row for c5's partitioned local step, which loads the state every round)
     uint32_t tw[TPL][8];
+    uint32_t ixr = 0;
+    if constexpr (PART) {  // (first: the env's scalars and its reply's place travel with the state batch)
+      eb_w = ld(P->eblk, (size_t)e * PART_EB + (uint32_t)lane);
+      ixr = ld(P->req_ix, (size_t)e);
+    }
 #pragma unroll
     for (int k = 0; k < TPL; ++k) {
       const size_t ti = tix(mine[k] ? lane + G * k : 0);
@@ -850,8 +850,15 @@ struct WEnv {
     }
     if constexpr (PART) {
       if (lane < 2 * SPL) ldirty[lane] = 0u;
-      // the env's scalars: one 64-lane load of its block (see sfl_part.h EB_*)
-      eb_w = ld(P->eblk, (size_t)e * PART_EB + (uint32_t)lane);
+      // the env's scalars: one 64-lane load of its block (see sfl_part.h EB_*), issued above
+      {  // the reply, if a request is open (a stale index of an env without one stays inside the buffer)
+        const uint32_t ix = U(ixr);
+        const vec_t<int32_t, 4> rw =
+            ld((const vec_t<int32_t, 4>*)(P->rep_in + (ix < P->world * (P->cap_req + 1u) ? ix : 0u)), 0);
+        rep_a = (uint32_t)rw[0];
+        rep_lo = (uint32_t)rw[2];
+        rep_hi = (uint32_t)rw[3];
+      }
       now = (int32_t)ebw(EB_ELAPSED);
       flags = ebw(EB_EFLAGS);
       epoch = ebw(EB_EPOCH);
@@ -1789,18 +1796,8 @@ struct WEnv {
       const double ud = Ud(pcg_double(rng));
       if (xp::kEpsConst) {
         explore = ud < m.eps0;
-      } else if (!SFL_AB_EPS_LOG) {
-        explore = ud < (n < (uint32_t)m.ntab ? LDC(m.eps_tab, (size_t)n) : m.eps0 * pow_ool(m.eps_decay, (double)n));
       } else {
-        // random() < eps0 * decay**n (distr_q.py:59-68, 314) decided in the log domain in single precision where
-        // that is certain -- log2(random()) more than 2^-10 away from log2(eps0) + n log2(decay), far beyond the
-        // f32 errors of both sides (< 1e-4 for n < 2^20) -- else on the host table's value itself (or pow past it):
-        // the same decision as the table's, without its load in the decision's chain (~1e-3 eps of draws fall
-        // back to it)
-        const float L = m.eps_l2a + (float)n * m.eps_l2b;
-        const float lu = __log2f((float)ud);
-        const bool yes = lu < L - 0x1p-10f, no = lu > L + 0x1p-10f;
-        explore = yes || (!no && eps_exact_ool(m.eps_tab, m.ntab, m.eps0, m.eps_decay, n, ud));
+        explore = ud < (n < (uint32_t)m.ntab ? LDC(m.eps_tab, (size_t)n) : m.eps0 * pow_ool(m.eps_decay, (double)n));
       }
       if (explore && !observe_only) {
         const uint32_t sub_seed = pcg_bounded(rng, 2147483646u);
@@ -1853,10 +1850,8 @@ struct WEnv {
     int best, arg;
     if (PART && !loc) {
       // the owner's reply: max over the full row, and the masked argmax (-1 for an exploratory request)
-      const uint32_t ix = U(ld(P->req_ix, (size_t)e));
-      const vec_t<int32_t, 4> rw = ld((const vec_t<int32_t, 4>*)(P->rep_in + ix), 0);
-      best = arg = U(rw[0]);
-      mx = __longlong_as_double(((long long)(uint32_t)U(rw[3]) << 32) | (long long)(uint32_t)U(rw[2]));
+      best = arg = U((int)rep_a);
+      mx = __longlong_as_double(((long long)U(rep_hi) << 32) | (long long)U(rep_lo));
     } else if (row_hit) {
       mx = Ud(pf_mx);
       const uint32_t ba = U(pfd23[0]) >> 16;
