@@ -98,9 +98,12 @@ def cpu_baseline(cm, seconds: float, config: str = "c3"):
                        f"after one untimed 64-decision step")
 
 
-def cpu_oracle_baseline(sc, seconds: float):
+def cpu_oracle_baseline(sc, seconds: float, check=None):
     """Second data point: the CPU oracle (pure-Python restatement of the reference loop, the
-    reference's own speed class), one env, one core."""
+    reference's own speed class), one env, one core.  check = (cm, device, group_lanes): afterwards the
+    product kernel runs the same env (seed, map, hyper-parameters) for the same decisions at the bench's
+    group size, and its Q-table must equal the oracle's (the reference's q_table dict) -- the bench line's
+    own oracle parity on exactly the sample it timed."""
     from oracle import sfl_oracle as so
     env, model = so.build(sc, 450565, HP, trace=False)
     state = None
@@ -110,9 +113,35 @@ def cpu_oracle_baseline(sc, seconds: float):
         n += 100
         state = so.run_decisions(model, n, state)
     dt = time.perf_counter() - t0
-    return dict(value=n / dt, unit="agent-env-steps/sec", cores=1, kind="port",
-                sample=f"oracle/sfl_oracle.py learn loop, 1 env of the c3 map, {n} decisions in {dt:.1f} s "
-                       f"(from episode start, incl. the Q-table init)")
+    out = dict(value=n / dt, unit="agent-env-steps/sec", cores=1, kind="port",
+               sample=f"oracle/sfl_oracle.py learn loop, 1 env of the {sc.name if hasattr(sc, 'name') else 'bench'} "
+                      f"map, {n} decisions in {dt:.1f} s (from episode start, incl. the Q-table init)")
+    if check is not None:
+        cm, device, g = check
+        runtime = importlib.import_module(PKG + ".runtime")
+        old = os.environ.get("SFL_WAVE_G")
+        os.environ["SFL_WAVE_G"] = str(g)  # (the bench kernel's shape, not the one-env batch's default)
+        try:
+            b = runtime.Batch(cm, HP, [450565], device=device)
+        finally:
+            if old is None:
+                os.environ.pop("SFL_WAVE_G", None)
+            else:
+                os.environ["SFL_WAVE_G"] = old
+        try:
+            b.learn_begin()
+            b.apply_qinit()
+            b.step(n)
+            c = b.counters()
+            same = b.q_dict(0) == model.q
+            out["oracle_parity"] = {
+                "result": "ok" if same else "FAIL",
+                "what": f"the product kernel (k_wave variant {c['kernel_variant']}, {c['group_lanes']} lanes per env) on "
+                        f"the same env for the same {n} decisions: Q-table (the reference's q_table dict) equal to "
+                        "the oracle's" + ("" if same else " -- it is not")}
+        finally:
+            b.close()
+    return out
 
 
 def visible_gpus() -> int:
@@ -404,7 +433,8 @@ def main():
             res["roofline"] = None
         if world == 1 and not args.no_cpu and not host:
             res["cpu_baseline"] = cpu_baseline(cm, args.cpu_seconds, args.config)
-            res["cpu_oracle_baseline"] = cpu_oracle_baseline(sc, args.cpu_seconds / 2)
+            res["cpu_oracle_baseline"] = cpu_oracle_baseline(sc, args.cpu_seconds / 2,
+                                                             check=(cm, dev, cnt0["group_lanes"]))
         print(json.dumps(res), flush=True)
     b.close()
     if dist is not None:

@@ -293,7 +293,8 @@ def test_two_rank_partition_gpu_rounds_queue_between_checkpoints(lib):
     from tests import test_partition
     for st in test_partition.two_rank_run("c5", gpu=True, world=2, steps=(1024,), log_rounds=True):
         s = st[1024]
-        assert s["rounds"] >= 1025 and s["reads"] == s["checkpoints"]
+        # (k_wave decides on each rank's own rows in place, so a step takes fewer rounds than decisions + 1)
+        assert s["reads"] == s["checkpoints"] <= 8 + s["rounds"] // 32
 
 
 def test_two_rank_partition_gpu_deferred_envs_bit_equal(lib):
