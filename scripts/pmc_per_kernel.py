@@ -11,7 +11,7 @@ import sys
 
 
 def short(name):
-    name = re.sub(r"\(.*$", "", name)
+    name = re.sub(r"\(.*$", "", name.replace("(anonymous namespace)::", ""))
     m = re.search(r"(k_[a-z0-9_]+)(<[^>]*>)?", name)
     return (m.group(1) + (m.group(2) or "")) if m else name
 
