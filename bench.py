@@ -300,7 +300,7 @@ def main():
     ap.add_argument("--config", default="c3")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--verify-envs", type=int, default=8,
+    ap.add_argument("--verify-envs", type=int, default=32,
                     help="envs per rank re-run on the host build after timing and compared bit-exactly (0: none)")
     ap.add_argument("--experimental", action="store_true",
                     help="accept a tuning / experiment build as SFL_LIB (its defines are reported; SFL_X_* / SFL_AB_* "
@@ -390,6 +390,7 @@ def main():
     if args.verify_envs > 0:
         checked, bad = verify_fused(b, cm, seeds, [args.decisions] * (args.warmup + args.steps), args.verify_envs)
     pfield = parity_field(dist, checked, bad, device=red_dev)
+    res = None
     if rank == 0:
         avg_ms = kms / max(1, args.steps)
         bytes_per_launch = abytes / max(1, args.steps)
@@ -435,8 +436,19 @@ def main():
             res["cpu_baseline"] = cpu_baseline(cm, args.cpu_seconds, args.config)
             res["cpu_oracle_baseline"] = cpu_oracle_baseline(sc, args.cpu_seconds / 2,
                                                              check=(cm, dev, cnt0["group_lanes"]))
-        print(json.dumps(res), flush=True)
     b.close()
+    printed = []
+
+    def emit(r):
+        if not printed:
+            printed.append(1)
+            print(json.dumps(r), flush=True)
+    if world > 1 and not host and os.environ.get("SFL_NO_PARTITION_LEG") != "1":
+        leg = partition_leg(par, dist, world, rank, dev, red_dev, devices, res, emit)
+        if rank == 0:
+            res["partition_leg"] = leg
+    if rank == 0:
+        emit(res)
     if dist is not None:
         dist.destroy_process_group()
 
@@ -447,23 +459,33 @@ def bench_partition(args):
     Q bytes per GPU fixed).  A step = every env makes --decisions decisions = decisions + 1 message rounds."""
     import torch
     par = importlib.import_module(PKG + ".parallel")
-    part = importlib.import_module(PKG + ".partition")
     world, rank, local = par.world()
     if args.rehearse_on_host:
         raise SystemExit("bench.py: --rehearse-on-host covers the env-sharded bench, not --partition")
     dist, dev, red_dev = dist_setup(par, local)
     torch.cuda.set_device(dev)
     devices = rank_devices(dist, dev, device=red_dev)
+    if rank == 0:
+        importlib.import_module(PKG + ".build").build_hip()
+    if dist is not None:
+        dist.barrier()
+    res = partition_run(args, par, dist, world, rank, dev, red_dev, devices)
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def partition_run(args, par, dist, world, rank, dev, red_dev, devices):
+    """The partitioned bench on the ranks of `dist` (collective); the bench line's dict on rank 0, else None."""
+    import torch
+    part = importlib.import_module(PKG + ".partition")
     mapgen = importlib.import_module(PKG + ".mapgen")
     comp = importlib.import_module(PKG + ".compiler")
     cfg = args.config if args.config != "c3" else "c5"
     E = args.envs if args.envs != 65536 else 16384
     cm = comp.compile_scenario(mapgen.make_config(cfg))
     seeds = par.shard_seeds(450565, E, rank)
-    if rank == 0:
-        importlib.import_module(PKG + ".build").build_hip()
-    if dist is not None:
-        dist.barrier()
     local = not args.remote_rows
     if args.virtual_ranks > 1 and world == 1 and local:
         local = (part.partition_switches(cm, args.virtual_ranks) == 0).astype(np.uint8)
@@ -504,6 +526,7 @@ def bench_partition(args):
                                      host)
         checked = len(pick)
     pfield = parity_field(dist, checked, bad, device=red_dev)
+    res = None
     if rank == 0:
         res = {
             "metric": METRIC,
@@ -542,10 +565,46 @@ def bench_partition(args):
             "devices": devices,
             **pfield,
         }
-        print(json.dumps(res), flush=True)
     pb.close()
-    if dist is not None:
-        dist.destroy_process_group()
+    return res
+
+
+# configs[4] inside every N > 1 run of the default bench: the driver launches bench.py itself under
+# torch.distributed.run, so this is where the partitioned exchange meets RCCL on a multi-GPU node.  A short run
+# (c5, 2,048 envs per GPU, 64 decisions per step), after the env-sharded measurement, parity-checked like
+# --partition; a watchdog keeps a hang from costing the bench line (rank 0 prints it with the leg's error, then
+# every rank exits).  SFL_NO_PARTITION_LEG=1 skips it.
+PARTITION_LEG = dict(config="c5", envs=2048, decisions=64, steps=2, warmup=1, verify_envs=2, remote_rows=False,
+                     virtual_ranks=0)
+PARTITION_LEG_TIMEOUT_S = 300.0
+
+
+def partition_leg(par, dist, world, rank, dev, red_dev, devices, res, emit):
+    """Run PARTITION_LEG on every rank; on rank 0 return its summary for the bench line."""
+    import threading
+    def fire():
+        if rank == 0:
+            res["partition_leg"] = {"error": f"no result within {PARTITION_LEG_TIMEOUT_S:.0f} s; the bench line "
+                                             "was printed by the watchdog"}
+            emit(res)
+        os._exit(0)
+    timer = threading.Timer(PARTITION_LEG_TIMEOUT_S, fire)
+    timer.daemon = True
+    timer.start()
+    t0 = time.perf_counter()
+    try:
+        leg = partition_run(argparse.Namespace(**PARTITION_LEG), par, dist, world, rank, dev, red_dev, devices)
+    finally:
+        timer.cancel()
+    if rank != 0:
+        return None
+    cfgd = leg["config"]
+    return {"what": "configs[4] at this N: " + cfgd["workload"] + f", {PARTITION_LEG['steps']} timed steps",
+            "value": leg["value"], "unit": leg["unit"], "backend": leg["backend"], "world_size": leg["world_size"],
+            "rounds_per_step": cfgd["rounds_per_step"], "checkpoints_per_step": cfgd["checkpoints_per_step"],
+            "count_reads_per_step": cfgd["count_reads_per_step"], "segment_records": cfgd["segment_records"],
+            "deferrals": cfgd["deferrals"], "parity": leg.get("parity"),
+            "parity_envs_checked": leg.get("parity_envs_checked"), "wall_s": time.perf_counter() - t0}
 
 
 if __name__ == "__main__":

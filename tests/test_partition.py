@@ -276,3 +276,24 @@ def test_error_on_one_rank_stops_every_rank():
     for p in procs:
         p.join(timeout=60)
     assert res == [(r, "raised") for r in range(world)], res
+
+
+def test_segment_caps_validated_and_resized():
+    """sfl_part_set_caps refuses capacities outside [1, configured]; the checkpoint rule grows k at once to
+    cover the peak demand with a margin, keeps it while the demand fits, and shrinks it below half."""
+    _lib = importlib.import_module("network-distributed-q-learning_amd._lib")
+    cm = comp.compile_scenario(mapgen.make_config("c2"))
+    pb = part.PartitionedBatch(cm, HP, [450565 + i for i in range(4)], 0, 4, lib=hostsim.lib(), ntab=4096,
+                               buffer_device="cpu")
+    for bad in ((0, 8), (pb.cap_req + 1, 8), (1, 0), (1, pb.cap_upd + 1)):
+        with pytest.raises(_lib.SflError):
+            pb.set_caps(*bad)
+    pb.set_caps(2, 3)
+    assert (pb.k_req, pb.k_upd) == (2, 3)
+    pb.close()
+    rs = part.PartitionedBatch._resize
+    assert rs(16, 100, 10_000) == 144          # grow: 100 + 25 + 16, rounded up to 16
+    assert rs(144, 100, 10_000) == 144         # demand fits: keep
+    assert rs(144, 40, 10_000) == 144          # 2 x 80 >= 144: keep
+    assert rs(144, 20, 10_000) == 48           # below half: shrink
+    assert rs(16, 100, 64) == 64               # never beyond the configured capacity
