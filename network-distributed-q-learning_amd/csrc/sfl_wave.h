@@ -375,6 +375,10 @@ struct WEnv {
   // PART: switches whose counter changed in this launch, a bitmap of (G * SPL) / 32 words after lsem0 (cset sets
   // the bit; store() writes back only those counters)
   uint32_t* ldirty = nullptr;
+  // PART: the launch's loaded train records, [TPL][6][64] words (pos, bits, plan, next | prev, src | dec, delay)
+  // after ldirty: store() writes back only the fields that changed (a round moves few trains; round 3 wrote all
+  // eight arrays of every train, ~50 of the 60 write requests per env and round)
+  uint32_t* ltr0 = nullptr;
   // PART: this lane's word of the env's scalar block (SflPart::eblk; lane i holds word i), loaded by load()
   uint32_t eb_w = 0;
   // PART: the reply to the env's last request (action, max lo / hi words), loaded by load() right behind the
@@ -824,6 +828,15 @@ struct WEnv {
         nprv[k] = tw[k][3] | (tw[k][4] << 16);
         sdec[k] = tw[k][5] | (tw[k][6] << 16);
         delay[k] = (int32_t)tw[k][7];
+        if constexpr (PART) {
+          uint32_t* t0 = ltr0 + (k * 6) * 64 + lane;
+          t0[0] = (uint32_t)pos[k];
+          t0[64] = bits[k];
+          t0[128] = plan[k];
+          t0[192] = nprv[k];
+          t0[256] = sdec[k];
+          t0[320] = (uint32_t)delay[k];
+        }
         if constexpr (!PART) {
           *(vec_t<int32_t, 4>*)(ltt + 8 * hk) = ld((const vec_t<int32_t, 4>*)m.tr_pack, (size_t)hk * 2u);
           *(vec_t<int32_t, 4>*)(ltt + 8 * hk + 4) = ld((const vec_t<int32_t, 4>*)m.tr_pack, (size_t)hk * 2u + 1u);
@@ -911,8 +924,28 @@ struct WEnv {
   }
   // returns the env's error bits (OR over lanes); PART writes its scalars with store_eblk
   __device__ __forceinline__ uint32_t store(int32_t phase) {
+    if constexpr (PART) {  // only the changed fields (the LDS reads first, then the stores)
+      uint32_t o[TPL][6];
 #pragma unroll
-    for (int k = 0; k < TPL; ++k) {
+      for (int k = 0; k < TPL; ++k)
+#pragma unroll
+        for (int i = 0; i < 6; ++i) o[k][i] = ltr0[(k * 6 + i) * 64 + lane];
+#pragma unroll
+      for (int k = 0; k < TPL; ++k) {
+        const int hk = lane + G * k;
+        if (!mine[k]) continue;
+        if ((uint32_t)pos[k] != o[k][0]) st(s.tr_pos, tix(hk), pos[k]);
+        if (bits[k] != o[k][1]) st(s.tr_bits, tix(hk), bits[k]);
+        if (plan[k] != o[k][2]) st(s.tr_plan, tix(hk), plan[k]);
+        if ((nprv[k] ^ o[k][3]) & 0xFFFFu) st(s.tr_next, tix(hk), (uint16_t)(nprv[k] & 0xFFFFu));
+        if ((nprv[k] ^ o[k][3]) >> 16) st(s.tr_prev, tix(hk), (uint16_t)(nprv[k] >> 16));
+        if ((sdec[k] ^ o[k][4]) & 0xFFFFu) st(s.tr_src, tix(hk), (uint16_t)(sdec[k] & 0xFFFFu));
+        if ((sdec[k] ^ o[k][4]) >> 16) st(s.tr_dec, tix(hk), (uint16_t)(sdec[k] >> 16));
+        if ((uint32_t)delay[k] != o[k][5]) st(s.tr_delay, tix(hk), delay[k]);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < TPL && !PART; ++k) {
       const int hk = lane + G * k;
       if (mine[k]) {
         st(s.tr_pos, tix(hk), pos[k]);
@@ -2280,7 +2313,8 @@ __device__ void run(const SflMap& m, const SflState& s, const SflCtl& c, const S
   using V = WEnv<PPL, SPL, TW, PART>;
   // semaphores, counters, prefetch records, rng, timetable (PART: one record, timetable from the map)
   // (PART: the launch's initial records / counters in place of the timetable copy)
-  constexpr int LDS_WORDS = 64 * (PPL + SPL) + V::PF_SLOTS * PF_WORDS + 12 + (PART ? 64 * PPL + 2 * SPL : TW * 8);
+  constexpr int LDS_WORDS =
+      64 * (PPL + SPL) + V::PF_SLOTS * PF_WORDS + 12 + (PART ? 64 * PPL + 2 * SPL + 6 * 64 * V::TPL : TW * 8);
   const int lane = (int)__lane_id();
   const uint32_t e = uni((uint32_t)((blockIdx.x * blockDim.x + threadIdx.x) >> 6));
   if (e >= s.E) return;
@@ -2290,6 +2324,7 @@ __device__ void run(const SflMap& m, const SflState& s, const SflCtl& c, const S
   if constexpr (PART) {
     v.lsem0 = lds + (threadIdx.x >> 6) * LDS_WORDS + 64 * (PPL + SPL) + V::PF_SLOTS * PF_WORDS + 12;
     v.ldirty = v.lsem0 + 64 * PPL;
+    v.ltr0 = v.ldirty + 2 * SPL;
   }
   PhaseTimer tm;
   if constexpr (TIMED) tm.start(c.phase_cyc != nullptr && blockIdx.x % TM_SAMPLE == 0u);
