@@ -443,8 +443,8 @@ def main():
         if not printed:
             printed.append(1)
             print(json.dumps(r), flush=True)
-    if world > 1 and not host and os.environ.get("SFL_NO_PARTITION_LEG") != "1":
-        leg = partition_leg(par, dist, world, rank, dev, red_dev, devices, res, emit)
+    if world > 1 and os.environ.get("SFL_NO_PARTITION_LEG") != "1":
+        leg = partition_leg(par, dist, world, rank, dev, red_dev, devices, res, emit, host=host)
         if rank == 0:
             res["partition_leg"] = leg
     if rank == 0:
@@ -460,24 +460,26 @@ def bench_partition(args):
     import torch
     par = importlib.import_module(PKG + ".parallel")
     world, rank, local = par.world()
-    if args.rehearse_on_host:
-        raise SystemExit("bench.py: --rehearse-on-host covers the env-sharded bench, not --partition")
-    dist, dev, red_dev = dist_setup(par, local)
-    torch.cuda.set_device(dev)
-    devices = rank_devices(dist, dev, device=red_dev)
+    host = args.rehearse_on_host
+    dist, dev, red_dev = dist_setup(par, local, host)
+    if not host:
+        torch.cuda.set_device(dev)
+    devices = rank_devices(dist, -1 if host else dev, device=red_dev)
     if rank == 0:
-        importlib.import_module(PKG + ".build").build_hip()
+        build = importlib.import_module(PKG + ".build")
+        build.build_hostsim() if host else build.build_hip()
     if dist is not None:
         dist.barrier()
-    res = partition_run(args, par, dist, world, rank, dev, red_dev, devices)
+    res = partition_run(args, par, dist, world, rank, dev, red_dev, devices, host=host)
     if rank == 0:
         print(json.dumps(res), flush=True)
     if dist is not None:
         dist.destroy_process_group()
 
 
-def partition_run(args, par, dist, world, rank, dev, red_dev, devices):
-    """The partitioned bench on the ranks of `dist` (collective); the bench line's dict on rank 0, else None."""
+def partition_run(args, par, dist, world, rank, dev, red_dev, devices, host: bool = False):
+    """The partitioned bench on the ranks of `dist` (collective); the bench line's dict on rank 0, else None.
+    host: the --rehearse-on-host run (the host build of the kernel body, CPU buffers, gloo)."""
     import torch
     part = importlib.import_module(PKG + ".partition")
     mapgen = importlib.import_module(PKG + ".mapgen")
@@ -489,8 +491,13 @@ def partition_run(args, par, dist, world, rank, dev, red_dev, devices):
     local = not args.remote_rows
     if args.virtual_ranks > 1 and world == 1 and local:
         local = (part.partition_switches(cm, args.virtual_ranks) == 0).astype(np.uint8)
+    lib = None
+    if host:
+        _lib = importlib.import_module(PKG + "._lib")
+        lib = _lib.Lib(importlib.import_module(PKG + ".build").build_hostsim())
+        lib.check_fresh()
     pb = part.PartitionedBatch(cm, HP, seeds, rank * E, world * E, rank=rank, world=world, dist=dist, device=dev,
-                               buffer_device="cuda", local_rows=local)
+                               lib=lib, buffer_device="cpu" if host else "cuda", local_rows=local)
     pb.learn_begin()
     pb.apply_qinit()
     for _ in range(args.warmup):
@@ -499,7 +506,8 @@ def partition_run(args, par, dist, world, rank, dev, red_dev, devices):
     def barrier():
         if dist is not None:
             dist.barrier()
-        torch.cuda.synchronize()
+        if not host:
+            torch.cuda.synchronize()
 
     barrier()
     t0 = time.perf_counter()
@@ -556,7 +564,8 @@ def partition_run(args, par, dist, world, rank, dev, red_dev, devices):
                        "checkpoints_per_step": (pb.checkpoints - ck0) / max(1, args.steps),
                        "host_waits_per_step": (w1 - w0) / max(1, args.steps),
                        "count_reads_per_step": (r1 - r0) / max(1, args.steps),
-                       "segment_records": [pb.k_req, pb.k_upd], "segment_capacity": [pb.cap_req, pb.cap_upd],
+                       "segment_records": pb.k_msg, "segment_capacity": pb.cap_msg,
+                       "collectives_per_round": 2 if world > 1 else 0,
                        "deferrals": pb.deferrals - d0,
                        "parallelism": f"env-batch dp{world} x switch-agent partition {world}"},
             "library": library_info(pb.lib),
@@ -565,6 +574,8 @@ def partition_run(args, par, dist, world, rank, dev, red_dev, devices):
             "devices": devices,
             **pfield,
         }
+        if host:
+            res["rehearsal"] = "host build of the kernel body over gloo: a rehearsal, not a GPU measurement"
     pb.close()
     return res
 
@@ -572,39 +583,63 @@ def partition_run(args, par, dist, world, rank, dev, red_dev, devices):
 # configs[4] inside every N > 1 run of the default bench: the driver launches bench.py itself under
 # torch.distributed.run, so this is where the partitioned exchange meets RCCL on a multi-GPU node.  A short run
 # (c5, 2,048 envs per GPU, 64 decisions per step), after the env-sharded measurement, parity-checked like
-# --partition; a watchdog keeps a hang from costing the bench line (rank 0 prints it with the leg's error, then
-# every rank exits).  SFL_NO_PARTITION_LEG=1 skips it.
+# --partition.  A failure of the leg must not cost the bench line, and must not look like success either: rank 0
+# prints the line with the leg's error and every rank exits with PARTITION_LEG_FAILED -- on an exception at once
+# (rank 0) or after the watchdog (the other ranks wait for it, so that the launcher does not stop rank 0 before it
+# has printed), on a hang by the watchdog (rank 0 first).  SFL_NO_PARTITION_LEG=1 skips it.  --rehearse-on-host
+# runs it on the host build (PARTITION_LEG_HOST).
 PARTITION_LEG = dict(config="c5", envs=2048, decisions=64, steps=2, warmup=1, verify_envs=2, remote_rows=False,
                      virtual_ranks=0)
+PARTITION_LEG_HOST = dict(PARTITION_LEG, envs=4, decisions=24, steps=1)
 PARTITION_LEG_TIMEOUT_S = 300.0
+PARTITION_LEG_FAILED = 3
 
 
-def partition_leg(par, dist, world, rank, dev, red_dev, devices, res, emit):
+def _hold_then_exit(seconds: float):
+    """A rank other than 0 whose leg failed: wait (for rank 0's line), then end with the failure code."""
+    time.sleep(seconds)
+    os._exit(PARTITION_LEG_FAILED)
+
+
+def partition_leg(par, dist, world, rank, dev, red_dev, devices, res, emit, host: bool = False):
     """Run PARTITION_LEG on every rank; on rank 0 return its summary for the bench line."""
     import threading
-    def fire():
+    timeout = PARTITION_LEG_TIMEOUT_S + (0.0 if rank == 0 else 30.0)  # (rank 0's fires first)
+
+    def fail(error):
         if rank == 0:
-            res["partition_leg"] = {"error": f"no result within {PARTITION_LEG_TIMEOUT_S:.0f} s; the bench line "
-                                             "was printed by the watchdog"}
+            res["partition_leg"] = {"error": error}
             emit(res)
-        os._exit(0)
-    timer = threading.Timer(PARTITION_LEG_TIMEOUT_S, fire)
+        os._exit(PARTITION_LEG_FAILED)
+    timer = threading.Timer(timeout, fail, args=(f"no result within {PARTITION_LEG_TIMEOUT_S:.0f} s; the bench "
+                                                 "line was printed by the watchdog",))
     timer.daemon = True
     timer.start()
     t0 = time.perf_counter()
+    spec = PARTITION_LEG_HOST if host else PARTITION_LEG
     try:
-        leg = partition_run(argparse.Namespace(**PARTITION_LEG), par, dist, world, rank, dev, red_dev, devices)
-    finally:
-        timer.cancel()
+        leg = partition_run(argparse.Namespace(**spec), par, dist, world, rank, dev, red_dev, devices, host=host)
+    except Exception as ex:  # noqa: BLE001 -- reported on the line and in the exit code
+        print(f"bench.py: rank {rank}: the partitioned leg failed: {ex!r}", file=sys.stderr, flush=True)
+        if rank == 0:
+            timer.cancel()
+            fail(f"rank 0: {ex!r}")
+            return None  # (only when os._exit is replaced, in tests)
+        return _hold_then_exit(max(0.0, timeout - (time.perf_counter() - t0)))
+    timer.cancel()
     if rank != 0:
         return None
     cfgd = leg["config"]
-    return {"what": "configs[4] at this N: " + cfgd["workload"] + f", {PARTITION_LEG['steps']} timed steps",
-            "value": leg["value"], "unit": leg["unit"], "backend": leg["backend"], "world_size": leg["world_size"],
-            "rounds_per_step": cfgd["rounds_per_step"], "checkpoints_per_step": cfgd["checkpoints_per_step"],
-            "count_reads_per_step": cfgd["count_reads_per_step"], "segment_records": cfgd["segment_records"],
-            "deferrals": cfgd["deferrals"], "parity": leg.get("parity"),
-            "parity_envs_checked": leg.get("parity_envs_checked"), "wall_s": time.perf_counter() - t0}
+    out = {"what": "configs[4] at this N: " + cfgd["workload"] + f", {spec['steps']} timed step(s)",
+           "value": leg["value"], "unit": leg["unit"], "backend": leg["backend"], "world_size": leg["world_size"],
+           "rounds_per_step": cfgd["rounds_per_step"], "checkpoints_per_step": cfgd["checkpoints_per_step"],
+           "count_reads_per_step": cfgd["count_reads_per_step"], "segment_records": cfgd["segment_records"],
+           "collectives_per_round": cfgd.get("collectives_per_round"),
+           "deferrals": cfgd["deferrals"], "parity": leg.get("parity"),
+           "parity_envs_checked": leg.get("parity_envs_checked"), "wall_s": time.perf_counter() - t0}
+    if host:
+        out["rehearsal"] = leg.get("rehearsal")
+    return out
 
 
 if __name__ == "__main__":

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define SFL_ABI_VERSION 7
+#define SFL_ABI_VERSION 8
 
 typedef struct sfl_handle sfl_handle;
 
@@ -176,45 +176,45 @@ int sfl_mf_schedule_flatland(const uint32_t* key, int32_t nkey, const int32_t* w
  * The switch agents are partitioned over `world` ranks (owner[S]); rank r stores the Q rows of
  * the switches it owns for all `envs_total` envs of the job, and simulates its own envs
  * [env_base, env_base + n_envs).  A round: sfl_part_local (every local env applies the reply
- * to its last request, runs to its next decision and writes that decision's request, plus the
- * update records of its post step), an all-to-all of the update and request buffers,
- * sfl_part_update + sfl_part_answer on the received records, and an all-to-all of the replies
- * back.  Buffers are [world][k + 1] records (record 0 of a segment = header holding the count; k =
- * the capacities of sfl_part_set_caps, the configured ones until then); on the GPU they are device
- * pointers (the caller's RCCL buffers).  An env whose request or update records do not all fit
- * this round's segments is deferred whole: it sends nothing (its places below the segment end carry
- * void records), sits out the next sfl_part_local and sends the same records again -- so the
- * exchange has a fixed size and needs no counts, and results do not depend on the capacities.
+ * to its last request, runs to its next decision and stages that decision's request, plus the
+ * update records of its post step; the staged records are packed into one message segment per
+ * destination rank, each env's records for that rank as a contiguous group: its updates in the
+ * order it made them, then its request), ONE all-to-all of the message buffer, sfl_part_owner on
+ * the received segments (per group: the updates in order, then the answer to the request), and an
+ * all-to-all of the replies back.  Buffers are [world][k + 1] records (record 0 of a segment =
+ * header holding the count; k = the capacity of sfl_part_set_caps, cap_req + cap_upd until then):
+ * messages of sfl_part_record_sizes' `msg` bytes, replies of `rep` bytes, a reply at its request's
+ * record index; on the GPU they are device pointers (the caller's RCCL buffers).  An env whose group
+ * does not fit this round's segment is deferred whole: it sends nothing (its places below the
+ * segment end carry void records), sits out the next sfl_part_local and sends the same records
+ * again -- so the exchange has a fixed size and needs no counts, and results do not depend on k.
  * Replaces the reference's in-process successor lookup max_q(next_state, next_agent) and update
  * (switchfl/distr_q.py:419-466) across GPU boundaries. */
 int sfl_part_config(sfl_handle* h, int32_t rank, int32_t world, const int32_t* owner /* [S] */, uint32_t env_base,
                     uint32_t envs_total, uint32_t cap_req /* >= n_envs */, uint32_t cap_upd);
-int sfl_part_record_sizes(uint32_t* req, uint32_t* rep, uint32_t* upd);
+int sfl_part_record_sizes(uint32_t* msg, uint32_t* rep);
 int sfl_part_begin(sfl_handle* h);  /* start a part step: per-env decision counters to 0 */
 /* requests_sent: the envs with a request or deferred this round (null: see sfl_set_stream) */
-int sfl_part_local(sfl_handle* h, int64_t decisions_per_env, const void* replies, void* requests, void* updates,
+int sfl_part_local(sfl_handle* h, int64_t decisions_per_env, const void* replies, void* messages,
                    uint64_t* requests_sent /* null: see sfl_set_stream */);
-int sfl_part_update(sfl_handle* h, const void* updates);
-int sfl_part_answer(sfl_handle* h, const void* requests, void* replies);
-/* this rank's record counts of the last sfl_part_local: out[0 .. world) requests and
- * out[world .. 2 world) update records per destination (staged, sent or deferred), out[2 world] the
- * highest update stage sent; then, when cap allows (4 world + 4 words): out[2 world + 1 .. 3 world + 1)
- * and out[3 world + 1 .. 4 world + 1) the peaks of those two counts since the previous call,
- * out[4 world + 1] the envs with a request or deferred, out[4 world + 2] the envs deferred in that
- * round, out[4 world + 3] the deferrals since the previous call.  cap >= 2 * world + 1;
+int sfl_part_owner(sfl_handle* h, const void* messages, void* replies);
+/* this rank's record counts of the last sfl_part_local: out[0 .. world) message records per
+ * destination (staged, sent or deferred); then, when cap allows (2 world + 3 words): out[world .. 2 world)
+ * their peaks since the previous call, out[2 world] the envs with a request or deferred, out[2 world + 1]
+ * the envs deferred in that round, out[2 world + 2] the deferrals since the previous call.  cap >= world;
  * synchronises if sfl_part_local did not (and reports the envs' errors) */
 int sfl_part_counts(sfl_handle* h, uint32_t* out, int32_t cap);
-/* the segment capacities of the next rounds (records per destination, 1 <= k <= the configured
- * cap_req / cap_upd): every rank of the job sets the same values, at a point where no round is in
- * flight (the buffers of a round are [world][k + 1] records).  A smaller k moves fewer bytes per
- * round; an env that does not fit waits a round (see above). */
-int sfl_part_set_caps(sfl_handle* h, uint32_t k_req, uint32_t k_upd);
+/* the segment capacity of the next rounds (records per destination, 1 <= k <= cap_req + cap_upd):
+ * every rank of the job sets the same value, at a point where no round is in flight (the buffers of
+ * a round are [world][k + 1] records).  A smaller k moves fewer bytes per round; an env that does not
+ * fit waits a round (see above). */
+int sfl_part_set_caps(sfl_handle* h, uint32_t k_msg);
 /* how often the handle has waited for its device since create (stream / event synchronisations; 0 on
  * the host build) and read the round counts back (sfl_part_counts, sfl_part_local with requests_sent):
  * what a caller checks to see that its rounds queue without the host in the loop */
 int sfl_get_sync_count(sfl_handle* h, uint64_t* waits, uint64_t* count_reads);
 /* queue the handle's work on the caller's stream (a hipStream_t, e.g. torch's current stream,
- * which its RCCL collectives follow).  Then sfl_part_update / sfl_part_answer return without a
+ * which its RCCL collectives follow).  Then sfl_part_owner returns without a
  * synchronisation, and so does sfl_part_local when requests_sent is null (its counts are read by
  * sfl_part_counts): the rounds between two sfl_part_counts calls queue without a synchronisation.
  * null: the handle's own stream again */

@@ -12,7 +12,7 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 PRODUCT_LIB = os.path.join(HERE, "libsfl.so")
-ABI_VERSION = 7  # include/sfl.h SFL_ABI_VERSION
+ABI_VERSION = 8  # include/sfl.h SFL_ABI_VERSION
 
 P = C.POINTER
 
@@ -96,13 +96,12 @@ EXPORTS = {
     # graph-partitioned mode (partition.py)
     "sfl_part_config": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, P(C.c_int32), C.c_uint32, C.c_uint32,
                                   C.c_uint32, C.c_uint32]),
-    "sfl_part_record_sizes": (C.c_int, [P(C.c_uint32), P(C.c_uint32), P(C.c_uint32)]),
+    "sfl_part_record_sizes": (C.c_int, [P(C.c_uint32), P(C.c_uint32)]),
     "sfl_part_begin": (C.c_int, [C.c_void_p]),
-    "sfl_part_local": (C.c_int, [C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p, P(C.c_uint64)]),
-    "sfl_part_update": (C.c_int, [C.c_void_p, C.c_void_p]),
-    "sfl_part_answer": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
+    "sfl_part_local": (C.c_int, [C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, P(C.c_uint64)]),
+    "sfl_part_owner": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
     "sfl_part_counts": (C.c_int, [C.c_void_p, P(C.c_uint32), C.c_int32]),
-    "sfl_part_set_caps": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32]),
+    "sfl_part_set_caps": (C.c_int, [C.c_void_p, C.c_uint32]),
     "sfl_get_sync_count": (C.c_int, [C.c_void_p, P(C.c_uint64), P(C.c_uint64)]),
     "sfl_set_stream": (C.c_int, [C.c_void_p, C.c_void_p]),
     "sfl_part_set_local_rows": (C.c_int, [C.c_void_p, P(C.c_uint8)]),

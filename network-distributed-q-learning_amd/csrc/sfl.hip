@@ -90,8 +90,8 @@ k_wave2_part(const sfl::SflMap* __restrict__ m, const sfl::SflState* __restrict_
   sfl::wave::run<PPL, SPL, TW, false, true>(*m, *s, *c, P);
 }
 
-// graph-partitioned rounds (sfl_part.h): local env step (lane per env), segment headers,
-// owner-side answer and update (one thread per record)
+// graph-partitioned rounds (sfl_part.h): local env step (lane per env), compaction into the
+// message segments, owner side (one thread per env group)
 template <int NW>
 __global__ void __launch_bounds__(256) k_part_local(const sfl::SflMap* __restrict__ m, const sfl::SflState* __restrict__ s,
                                                     const sfl::SflCtl* __restrict__ c, const sfl::SflPart* __restrict__ P) {
@@ -99,26 +99,28 @@ __global__ void __launch_bounds__(256) k_part_local(const sfl::SflMap* __restric
   if (e < s->E) sfl::env_run_part<NW>(*m, *s, *c, *P, e);
 }
 // after the local step: pack each env's staged request and update records into the destination
-// segments (a block reserves its range per destination with one global atomic, the envs their
-// places in it with LDS atomics), and add the launch totals of the envs that ran into P->sums.  A
-// segment holds k_req requests / k_upd update records this round: an env with a record at or past
-// that place is deferred whole (F_DEFER; its places below it get void records, its staged records go
-// again next round and the local step skips it until then).  arrays: the lane-per-env body (its
-// scalars in the SflState / SflPart arrays), else the wave kernels' per-env blocks (eblk).
-__global__ void __launch_bounds__(256) k_part_compact(const sfl::SflPart* __restrict__ P, const sfl::SflState* __restrict__ s,
-                                                      const sfl::SflCtl* __restrict__ c, int arrays) {
-  constexpr int MAXU = sfl::PART_UPD_ENV_MAX;  // (register arrays: the loops over them are unrolled)
-  __shared__ uint32_t lreq[256], lupd[256], breq[256], bupd[256];
-  __shared__ unsigned long long lsum[4][4];
-  __shared__ uint32_t lmax, lopen, ldefer;
+// segments, each env's records for one destination as a contiguous group (sfl_part.h env_groups: its
+// updates in emission order, then its request) -- a block reserves its range per destination with one
+// global atomic, the envs their groups in it with LDS atomics -- and add the launch totals of the envs
+// that ran into P->sums.  A segment holds k_msg records this round: an env with a group that reaches past
+// that place is deferred whole (F_DEFER; its places below the end get void records, its staged records go
+// again next round and the local step skips it until then).  arrays: the lane-per-env body (its scalars in
+// the SflState / SflPart arrays), else the wave kernels' per-env blocks (eblk).
+__global__ void __launch_bounds__(64) k_part_compact(const sfl::SflPart* __restrict__ P, const sfl::SflState* __restrict__ s,
+                                                     const sfl::SflCtl* __restrict__ c, int arrays) {
+  constexpr int R = sfl::PART_GROUP_MAX;  // (register arrays: the loops over them are unrolled)
+  __shared__ uint32_t lmsg[256], bmsg[256];
+  __shared__ unsigned long long lsum[4];
+  __shared__ uint32_t lopen, ldefer;
   const int world = P->world;
-  for (int i = threadIdx.x; i < world; i += blockDim.x) lreq[i] = lupd[i] = 0u;
-  if (threadIdx.x == 0) lmax = lopen = ldefer = 0u;
+  for (int i = threadIdx.x; i < world; i += blockDim.x) lmsg[i] = 0u;
   __syncthreads();
   const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
   const bool valid = e < s->E;
   int rd = -1;
-  uint32_t kr = 0, nu = 0, ku[MAXU], du[MAXU], flags = 0;
+  uint32_t nu = 0, flags = 0, n = 0;
+  int32_t dst[R];
+  uint32_t rank[R], size[R], place[R];
   // the wave kernel's per-env words (its scalar block, sfl_part.h EB_*), or the lane kernel's arrays
   const uint32_t* eb = (valid && !arrays) ? P->eblk + (size_t)e * sfl::PART_EB : nullptr;
   auto eb64 = [&](int i) { return (unsigned long long)eb[i] | ((unsigned long long)eb[i + 1] << 32); };
@@ -126,18 +128,21 @@ __global__ void __launch_bounds__(256) k_part_compact(const sfl::SflPart* __rest
     flags = eb ? eb[sfl::EB_EFLAGS] : s->eflags[e];
     rd = eb ? (int)eb[sfl::EB_REQ_DST] : P->req_dst[e];
     nu = eb ? eb[sfl::EB_UPD_N] : P->upd_n[e];
-    if (rd >= 0) kr = atomicAdd(&lreq[rd], 1u);
+    n = sfl::env_groups(*P, e, rd, nu, dst, rank, size);
+    // a group's first record reserves the group; the others take their places behind it
+    uint32_t gb[R];
 #pragma unroll
-    for (int i = 0; i < MAXU; ++i) {
-      if ((uint32_t)i < nu) {
-        const sfl::PartUpd& u = P->upd_st[(size_t)e * P->upd_env + i];
-        du[i] = (uint32_t)P->owner[u.port >> 2];
-        ku[i] = atomicAdd(&lupd[du[i]], 1u);
-      }
+    for (int r = 0; r < R; ++r) gb[r] = ((uint32_t)r < n && rank[r] == 0u) ? atomicAdd(&lmsg[dst[r]], size[r]) : 0u;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      uint32_t b = 0;
+#pragma unroll
+      for (int q = 0; q < R; ++q) b += (rank[q] == 0u && dst[q] == dst[r]) ? gb[q] : 0u;
+      place[r] = b + rank[r];
     }
   }
   // the launch totals of the envs that ran (a deferred env sat the local step out: its totals are the
-  // last round's, already counted): wave sums, then one LDS slot per wave
+  // last round's, already counted): one wave per block
   const bool ran = valid && !(flags & sfl::F_DEFER);
   unsigned long long a = !ran ? 0ull : eb ? eb64(sfl::EB_L_DEC) : c->launch_dec[e],
                      b = !ran ? 0ull : eb ? eb64(sfl::EB_L_TICKS) : c->launch_ticks[e],
@@ -149,81 +154,53 @@ __global__ void __launch_bounds__(256) k_part_compact(const sfl::SflPart* __rest
     d += __shfl_xor(d, off, 64);
     o |= __shfl_xor(o, off, 64);
   }
-  if ((threadIdx.x & 63) == 0) {
-    const int w = threadIdx.x >> 6;
-    lsum[w][0] = a;
-    lsum[w][1] = b;
-    lsum[w][2] = d;
-    lsum[w][3] = o;
+  if (threadIdx.x == 0) {
+    lsum[0] = a;
+    lsum[1] = b;
+    lsum[2] = d;
+    lsum[3] = o;
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < world; i += blockDim.x) {
-    breq[i] = lreq[i] ? atomicAdd(P->cnt + i, lreq[i]) : 0u;
-    bupd[i] = lupd[i] ? atomicAdd(P->cnt + world + i, lupd[i]) : 0u;
-  }
+  for (int i = threadIdx.x; i < world; i += blockDim.x) bmsg[i] = lmsg[i] ? atomicAdd(P->cnt + i, lmsg[i]) : 0u;
   if (threadIdx.x < 4) {
-    unsigned long long t = 0;
-    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t = threadIdx.x == 3 ? (t | lsum[w][3]) : t + lsum[w][threadIdx.x];
+    const unsigned long long t = lsum[threadIdx.x];
     if (threadIdx.x == 3) {
       if (t) atomicOr((unsigned long long*)&P->sums[3], t);
-    } else {
+    } else if (t) {
       atomicAdd((unsigned long long*)&P->sums[threadIdx.x], t);
     }
   }
-  __syncthreads();  // (breq / bupd: this block's reservations)
-  // does every record of the env fit this round's segments?
-  const uint32_t kq = P->k_req, kup = P->k_upd;
+  __syncthreads();  // (bmsg: this block's reservations)
+  // does every group of the env fit this round's segments?
+  const uint32_t k = P->k_msg;
   bool fits = valid;
-  uint32_t mst = 0;
-  if (valid) {
-    if (rd >= 0 && breq[rd] + kr >= kq) fits = false;
 #pragma unroll
-    for (int i = 0; i < MAXU; ++i)
-      if ((uint32_t)i < nu && bupd[du[i]] + ku[i] >= kup) fits = false;
-    if (fits)
-#pragma unroll
-      for (int i = 0; i < MAXU; ++i)
-        if ((uint32_t)i < nu) mst = max(mst, (uint32_t)P->upd_st[(size_t)e * P->upd_env + i].stage);
-  }
+  for (int r = 0; r < R; ++r)
+    if ((uint32_t)r < n && bmsg[dst[r]] + place[r] >= k) fits = false;
   const bool deferred = valid && !fits;
   const bool open = valid && (rd >= 0 || deferred);
   const uint32_t n_open = __popcll(__ballot(open)), n_def = __popcll(__ballot(deferred));
-  for (int off = 32; off > 0; off >>= 1) mst = max(mst, (uint32_t)__shfl_xor((int)mst, off, 64));
-  if ((threadIdx.x & 63) == 0) {
-    if (n_open) atomicAdd(&lopen, n_open);
-    if (n_def) atomicAdd(&ldefer, n_def);
-    if (mst) atomicMax(&lmax, mst);
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    if (lopen) atomicAdd(P->cnt + 2 * world + 2, lopen);
-    if (ldefer) atomicAdd(P->cnt + 2 * world + 3, ldefer);
-    if (lmax) atomicMax(P->max_stage, lmax);
-  }
   // the last block to get here writes the segment headers and hands the counts and totals to the
   // host copy (zeroing them for the next round): every block's reservations are done by then
   __shared__ bool last;
+  if (threadIdx.x == 0) {
+    if (n_open) atomicAdd(P->cnt + world + 1, n_open);
+    if (n_def) atomicAdd(P->cnt + world + 2, n_def);
+  }
   __threadfence();  // (a workgroup-scope fence here measured +0.8 % on the C5 round; not worth the ordering risk)
   if (threadIdx.x == 0) last = atomicAdd(P->blocks_done, 1u) == gridDim.x - 1u;
   __syncthreads();
   if (last) {
     __threadfence();
     uint32_t* co = (uint32_t*)(P->cnt_out + 4);
-    const uint32_t top = atomicExch(P->max_stage, 0u);
     for (int i = threadIdx.x; i < world; i += blockDim.x) {
-      const uint32_t nr = atomicExch(P->cnt + i, 0u), nw = atomicExch(P->cnt + world + i, 0u);
-      P->req_out[(size_t)i * (kq + 1)].genv = nr < kq ? nr : kq;
-      sfl::PartUpd& hu = P->upd_out[(size_t)i * (kup + 1)];
-      hu.genv = nw < kup ? nw : kup;
-      hu.state = top;
-      co[sfl::PART_C_REQ(world) + i] = nr;
-      co[sfl::PART_C_UPD(world) + i] = nw;
-      co[sfl::PART_C_PEAK_REQ(world) + i] = max(co[sfl::PART_C_PEAK_REQ(world) + i], nr);
-      co[sfl::PART_C_PEAK_UPD(world) + i] = max(co[sfl::PART_C_PEAK_UPD(world) + i], nw);
+      const uint32_t nm = atomicExch(P->cnt + i, 0u);
+      P->msg_out[(size_t)i * (k + 1)].genv = nm < k ? nm : k;
+      co[sfl::PART_C_MSG(world) + i] = nm;
+      co[sfl::PART_C_PEAK(world) + i] = max(co[sfl::PART_C_PEAK(world) + i], nm);
     }
     if (threadIdx.x == 0) {
-      const uint32_t no = atomicExch(P->cnt + 2 * world + 2, 0u), nd = atomicExch(P->cnt + 2 * world + 3, 0u);
-      co[sfl::PART_C_STAGE(world)] = top;
+      const uint32_t no = atomicExch(P->cnt + world + 1, 0u), nd = atomicExch(P->cnt + world + 2, 0u);
       co[sfl::PART_C_OPEN(world)] = no;
       co[sfl::PART_C_DEFER(world)] = nd;
       co[sfl::PART_C_DEFER_SUM(world)] += nd;
@@ -233,30 +210,19 @@ __global__ void __launch_bounds__(256) k_part_compact(const sfl::SflPart* __rest
     }
   }
   if (!valid) return;
-  if (fits) {
-    if (rd >= 0) {
-      const uint32_t k = breq[rd] + kr;
-      P->req_out[(size_t)rd * (kq + 1) + 1 + k] = P->req_st[e];
-      P->req_ix[e] = (uint32_t)rd * (kq + 1) + 1u + k;  // (where its reply lands: the reply segments match)
-    }
 #pragma unroll
-    for (int i = 0; i < MAXU; ++i) {
-      if ((uint32_t)i < nu) P->upd_out[(size_t)du[i] * (kup + 1) + 1 + bupd[du[i]] + ku[i]] = P->upd_st[(size_t)e * P->upd_env + i];
-    }
-  } else {  // void records in the places below the segments' ends
-    if (rd >= 0 && breq[rd] + kr < kq) {
-      sfl::PartReq& r = P->req_out[(size_t)rd * (kq + 1) + 1 + breq[rd] + kr];
-      r.genv = 0u;
-      r.flags = sfl::REQ_VOID;
-    }
-#pragma unroll
-    for (int i = 0; i < MAXU; ++i) {
-      if ((uint32_t)i < nu && bupd[du[i]] + ku[i] < kup) {
-        sfl::PartUpd& u = P->upd_out[(size_t)du[i] * (kup + 1) + 1 + bupd[du[i]] + ku[i]];
-        u.genv = 0u;
-        u.stage = 0;
-        u.kind = sfl::UPD_VOID;
-      }
+  for (int r = 0; r < R; ++r) {
+    if ((uint32_t)r >= n) continue;
+    const uint32_t at = bmsg[dst[r]] + place[r];
+    sfl::PartMsg* x = P->msg_out + (size_t)dst[r] * (k + 1) + 1 + at;
+    if (fits) {
+      sfl::PartMsg y = (uint32_t)r < nu ? P->upd_st[(size_t)e * P->upd_env + r] : sfl::msg_of_req(P->req_st[e]);
+      y.kind |= rank[r] == 0u ? size[r] << 8 : 0u;
+      *x = y;
+      if ((uint32_t)r == nu) P->req_ix[e] = (uint32_t)dst[r] * (k + 1) + 1u + at;  // (its reply lands there)
+    } else if (at < k) {  // void records in the places below the segment's end
+      x->genv = 0u;
+      x->kind = sfl::MSG_VOID | (1u << 8);
     }
   }
   if ((bool)(flags & sfl::F_DEFER) != deferred) {
@@ -367,58 +333,25 @@ __device__ __forceinline__ void part_answer_fast(const sfl::SflMap& m, const sfl
   }
   out.action = arg;
 }
-__global__ void k_part_answer(const sfl::SflMap* __restrict__ m, const sfl::SflPart* __restrict__ P,
-                              const sfl::PartReq* __restrict__ in, sfl::PartRep* __restrict__ out) {
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const size_t cap = P->k_req;
-  const size_t g = i / cap, k = i % cap + 1;
-  if (g >= (size_t)P->world) return;
-  const size_t base = g * (cap + 1);
-  if (k > in[base].genv || in[base + k].flags == sfl::REQ_VOID) return;
-#ifdef SFL_ANSWER_GENERIC
-  sfl::part_answer_one(*m, *P, in[base + k], out[base + k]);  // (tuning A/B)
-#else
-  part_answer_fast(*m, *P, in[base + k], out[base + k]);
-#endif
-}
-// stage 0 (the pending updates and key-set inserts: one per env and cell) in parallel over a bounded grid
-// (a grid-stride loop to each segment's header count: the segments are sized for the worst case, 16 records
-// per env, a round fills ~1.5); the rare later stages (arrival bonuses) are listed for k_part_update_late.
-// (Round 3: merging the later stages into this kernel's last block cost 15 % of the round -- each block's
-// agent-scope release fence writes its XCD's L2 back, 512 times per round; the kernel boundary does it once.)
-__global__ void __launch_bounds__(256) k_part_update(const sfl::SflMap* __restrict__ m, const sfl::SflPart* __restrict__ P,
-                                                     const sfl::PartUpd* __restrict__ in) {
-  const size_t cap = P->k_upd, stride = (size_t)gridDim.x * blockDim.x;
+// owner side of a round: every received group (one env's records for this rank, sfl_part.h part_owner_group) by
+// one thread, in order -- the env's updates, then the answer to its request.  A grid-stride loop up to each
+// segment's header count (the grid is bounded: a segment may be sized for the worst case, 17 records per env).
+// Round 4 ran this as three kernels (stage-0 updates in parallel, the later stages in one block, then the
+// answers) because records of one env were spread over the segment; with an env's records contiguous no
+// ordering is needed across threads.
+__global__ void __launch_bounds__(256) k_part_owner(const sfl::SflMap* __restrict__ m, const sfl::SflPart* __restrict__ P,
+                                                    const sfl::PartMsg* __restrict__ in, sfl::PartRep* __restrict__ out) {
+  const size_t k = P->k_msg, stride = (size_t)gridDim.x * blockDim.x;
   for (int g = 0; g < P->world; ++g) {
-    const size_t base = (size_t)g * (cap + 1);
+    const size_t base = (size_t)g * (k + 1);
     const size_t n = in[base].genv;
-    for (size_t k = 1 + (size_t)blockIdx.x * blockDim.x + threadIdx.x; k <= n; k += stride) {
-      if (in[base + k].stage == 0) sfl::part_update_one(*m, *P, in[base + k]);
-      else P->late[1 + atomicAdd(P->late, 1u)] = (uint32_t)(base + k);
+    for (size_t i = 1 + (size_t)blockIdx.x * blockDim.x + threadIdx.x; i <= n; i += stride) {
+      const uint32_t len = sfl::msg_group(in[base + i].kind);
+      if (len == 0u || sfl::msg_type(in[base + i].kind) == sfl::MSG_VOID) continue;
+      sfl::part_owner_group(*m, *P, in + base + i, len, out + base + i,
+                            [&](const sfl::PartReq& r, sfl::PartRep& rep) { part_answer_fast(*m, *P, r, rep); });
     }
   }
-}
-// one block: the listed records stage by stage (a stage's records touch distinct cells of their
-// env; a later stage may revisit a cell), then the list is cleared for the next round
-__global__ void __launch_bounds__(1024) k_part_update_late(const sfl::SflMap* __restrict__ m, const sfl::SflPart* __restrict__ P,
-                                                           const sfl::PartUpd* __restrict__ in) {
-  const uint32_t n = P->late[0];
-  uint32_t top = 0;
-  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) top = max(top, (uint32_t)in[P->late[1 + i]].stage);
-  __shared__ uint32_t smax;
-  if (threadIdx.x == 0) smax = 0u;
-  __syncthreads();
-  atomicMax(&smax, top);
-  __syncthreads();
-  const uint32_t last = smax;
-  for (uint32_t st = 1; st <= last; ++st) {
-    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
-      const sfl::PartUpd& u = in[P->late[1 + i]];
-      if (u.stage == st) sfl::part_update_one(*m, *P, u);
-    }
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) P->late[0] = 0u;
 }
 __global__ void k_replicate(uint32_t* base, size_t words, uint32_t n) {
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < words * (n - 1); i += (size_t)gridDim.x * blockDim.x)
@@ -742,9 +675,9 @@ struct HipBackend {
     char p2[(sizeof(sfl::SflCtl) + 63) / 64 * 64 - sizeof(sfl::SflCtl)];
     sfl::SflPart P;
   };
-  // one device parameter block per round step (0 local, 1 answer, 2 update), uploaded only when
-  // its contents change: a round's three steps reuse the same buffers, so after the first round
-  // no step pays a host-to-device copy and its synchronisation
+  // one device parameter block per round step (0 local, 1 owner; 2 unused), uploaded only when
+  // its contents change: a round's steps reuse the same buffers, so after the first round no step
+  // pays a host-to-device copy and its synchronisation
   void* d_pparams = nullptr;
   PartParams pp_host[3];
   bool pp_valid[3] = {false, false, false};
@@ -775,8 +708,7 @@ struct HipBackend {
     bool any = false;
     for (int w = 0; w < 3; ++w) {
       if (!pp_valid[w]) continue;
-      pp_host[w].P.k_req = P.k_req;
-      pp_host[w].P.k_upd = P.k_upd;
+      pp_host[w].P.k_msg = P.k_msg;
       check(hipMemcpyAsync((char*)d_pparams + w * stride, &pp_host[w], sizeof(PartParams), hipMemcpyHostToDevice, stream),
             "params h2d");
       any = true;
@@ -816,32 +748,21 @@ struct HipBackend {
 #endif
     return err.empty() ? 0 : -1;
   }
-  void part_answer(const sfl::SflMap& m, const sfl::SflPart& P, const sfl::PartReq* in, sfl::PartRep* out) {
-    sfl::SflState s{};
-    sfl::SflCtl c{};
-    PartParams* pp = part_params(1, m, s, c, P);
-    if (!pp) return;
-    const size_t n = (size_t)P.world * P.k_req;
-    k_part_answer<<<(unsigned)((n + 63) / 64), 64, 0, stream>>>(&pp->m, &pp->P, in, out);
-    check(hipGetLastError(), "k_part_answer");
-  }
   // the wave kernels' per-env scalar blocks from / into the SflState arrays (k_part_eblk)
   void part_eblk(const sfl::SflState& s, const sfl::SflPart& P, int dir) {
     k_part_eblk<<<(s.E + 255) / 256, 256, 0, stream>>>(s, P.eblk, P.dec_done, dir);
     check(hipGetLastError(), "k_part_eblk");
   }
-  // every stage of the received update records, without the host knowing the highest stage
-  void part_update_all(const sfl::SflMap& m, const sfl::SflPart& P, const sfl::PartUpd* in) {
+  // the owner side of a round on the received message segments (k_part_owner)
+  void part_owner(const sfl::SflMap& m, const sfl::SflPart& P, const sfl::PartMsg* in, sfl::PartRep* out) {
     sfl::SflState s{};
     sfl::SflCtl c{};
-    PartParams* pp = part_params(2, m, s, c, P);
+    PartParams* pp = part_params(1, m, s, c, P);
     if (!pp) return;
-    const size_t n = (size_t)P.world * P.k_upd;
+    const size_t n = (size_t)P.world * P.k_msg;
     const unsigned blocks = (unsigned)std::min<size_t>((n + 255) / 256, 512);
-    k_part_update<<<blocks, 256, 0, stream>>>(&pp->m, &pp->P, in);
-    check(hipGetLastError(), "k_part_update");
-    k_part_update_late<<<1, 1024, 0, stream>>>(&pp->m, &pp->P, in);
-    check(hipGetLastError(), "k_part_update_late");
+    k_part_owner<<<blocks, 256, 0, stream>>>(&pp->m, &pp->P, in, out);
+    check(hipGetLastError(), "k_part_owner");
   }
 };
 

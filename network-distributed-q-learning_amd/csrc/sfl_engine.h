@@ -782,7 +782,8 @@ int part_config(Handle<B>* h, int rank, int world, const int32_t* owner, uint32_
   if (h->part.world) return fail("sfl_part_config: already configured");
   if (env_base + h->E > E_tot) return fail("sfl_part_config: env range outside envs_total");
   if (cap_req < h->E) return fail("sfl_part_config: request capacity must hold one request per local env");
-  if (cap_upd < 1 || (uint64_t)world * (cap_req + 1ull) >= (1ull << 32)) return fail("sfl_part_config: bad capacities");
+  if (cap_upd < 1 || (uint64_t)cap_req + cap_upd >= (1ull << 31) || (uint64_t)world * (cap_req + cap_upd + 1ull) >= (1ull << 32))
+    return fail("sfl_part_config: bad capacities");
   // the wave kernel stages up to upd_env update records per env and round (E_MSG_OVF beyond); the
   // segments must hold every env's staged records
   const uint32_t upd_env = cap_upd / h->E < PART_UPD_ENV_MAX ? cap_upd / h->E : PART_UPD_ENV_MAX;
@@ -818,10 +819,10 @@ int part_config(Handle<B>* h, int rank, int world, const int32_t* owner, uint32_
   P.world = world;
   P.env_base = env_base;
   P.E_tot = E_tot;
-  P.cap_req = cap_req;
-  P.cap_upd = cap_upd;
-  P.k_req = cap_req;  // (full segments until sfl_part_set_caps)
-  P.k_upd = cap_upd;
+  // a segment holds one group per env of a source rank: its request and its update records to this
+  // destination (cap_req >= the largest rank's env count, cap_upd its update records)
+  P.cap_msg = cap_req + cap_upd;
+  P.k_msg = P.cap_msg;  // (full segments until sfl_part_set_caps)
   P.q_own_per_env = off;
   P.own_rows = rows;
   P.own_words = (rows + 31u) / 32u;
@@ -836,7 +837,7 @@ int part_config(Handle<B>* h, int rank, int world, const int32_t* owner, uint32_
   P.obs = h->template dalloc<Obs>(h->E);
   P.req_ix = h->template dalloc<uint32_t>(h->E);
   P.dec_done = h->template dalloc<int64_t>(h->E);
-  P.cnt = h->template dalloc<uint32_t>(2 * (size_t)world + 4);
+  P.cnt = h->template dalloc<uint32_t>((size_t)world + 4);
   P.sums = h->d_sums;
   P.cnt_out = h->template dalloc<uint64_t>(4 + ((size_t)PART_NCNT(world) + 1) / 2);
   P.upd_env = upd_env;
@@ -844,17 +845,14 @@ int part_config(Handle<B>* h, int rank, int world, const int32_t* owner, uint32_
   P.req_dst = h->template dalloc<int32_t>(h->E);
   P.upd_st = h->template dalloc<PartUpd>((size_t)h->E * upd_env);
   P.upd_n = h->template dalloc<uint32_t>(h->E);
-  P.late = h->template dalloc<uint32_t>(1 + (size_t)world * cap_upd);
   P.eblk = nullptr;
   if (!P.owner || !P.q_own || !P.touched_own || !P.obs || !P.req_ix || !P.dec_done || !P.cnt || !P.cnt_out || !P.req_st ||
-      !P.req_dst || !P.upd_st || !P.upd_n || !P.late)
+      !P.req_dst || !P.upd_st || !P.upd_n)
     return fail("sfl_part_config: allocation failed (out of memory?)");
-  P.max_stage = P.cnt + 2 * world;
-  P.blocks_done = P.cnt + 2 * world + 1;
-  h->be.memset(P.cnt, 0, (2 * (size_t)world + 4) * 4);
+  P.blocks_done = P.cnt + world;
+  h->be.memset(P.cnt, 0, ((size_t)world + 4) * 4);
   h->be.memset(P.sums, 0, 4 * 8);
   h->be.memset(P.cnt_out, 0, (4 + ((size_t)PART_NCNT(world) + 1) / 2) * 8);
-  h->be.memset(P.late, 0, 4);
   h->be.fill_f64(P.q_own, h->map.default_q, (size_t)E_tot * off);
   h->be.memset(P.touched_own, 0, (size_t)E_tot * P.own_words * 4);
   h->be.memset(P.dec_done, 0, h->E * 8);
@@ -956,16 +954,14 @@ int part_begin(Handle<B>* h) {
   return h->be.sync() ? fail(h->be.error()) : 0;
 }
 
-// this round's segment sizes (records per destination, without the header): the buffers handed to the
-// next rounds hold [world][k + 1] records.  Every rank of the job must use the same values.
+// this round's segment size (records per destination, without the header): the buffers handed to the
+// next rounds hold [world][k + 1] records.  Every rank of the job must use the same value.
 template <class B>
-int part_set_caps(Handle<B>* h, uint32_t k_req, uint32_t k_upd) {
+int part_set_caps(Handle<B>* h, uint32_t k_msg) {
   SflPart& P = h->part;
   if (!P.world) return fail("sfl_part_set_caps: handle not partitioned");
-  if (k_req < 1 || k_req > P.cap_req || k_upd < 1 || k_upd > P.cap_upd)
-    return fail("sfl_part_set_caps: capacities outside [1, the configured capacity]");
-  P.k_req = k_req;
-  P.k_upd = k_upd;
+  if (k_msg < 1 || k_msg > P.cap_msg) return fail("sfl_part_set_caps: capacity outside [1, the configured capacity]");
+  P.k_msg = k_msg;
   h->be.part_caps(P);
   return h->be.error()[0] ? fail(std::string("sfl_part_set_caps: ") + h->be.error()) : 0;
 }
@@ -993,7 +989,7 @@ int part_read(Handle<B>* h) {
   if (!h->part_consumed) prev.swap(h->part_counts);  // (peaks and deferrals since sfl_part_counts: merged)
   h->part_counts.assign(cnt, cnt + PART_NCNT(W));
   if (prev.size() == h->part_counts.size()) {
-    for (int i = PART_C_PEAK_REQ(W); i < PART_C_OPEN(W); ++i) h->part_counts[i] = std::max(h->part_counts[i], prev[i]);
+    for (int i = PART_C_PEAK(W); i < PART_C_OPEN(W); ++i) h->part_counts[i] = std::max(h->part_counts[i], prev[i]);
     h->part_counts[PART_C_DEFER_SUM(W)] += prev[PART_C_DEFER_SUM(W)];
   }
   h->part_consumed = false;
@@ -1005,12 +1001,11 @@ int part_read(Handle<B>* h) {
 // the record counts and launch totals; without it on the caller's stream (sfl_set_stream), none:
 // sfl_part_counts reads them later (errors of the envs surface there)
 template <class B>
-int part_local(Handle<B>* h, int64_t budget, const void* rep_in, void* req_out, void* upd_out, uint64_t* n_req) {
+int part_local(Handle<B>* h, int64_t budget, const void* rep_in, void* msg_out, uint64_t* n_req) {
   SflPart& P = h->part;
   if (!P.world) return fail("sfl_part_local: handle not partitioned");
   P.rep_in = (const PartRep*)rep_in;
-  P.req_out = (PartReq*)req_out;
-  P.upd_out = (PartUpd*)upd_out;
+  P.msg_out = (PartMsg*)msg_out;
   SflCtl c{};
   c.mode = 0;
   c.ep_target = -1;
@@ -1037,20 +1032,14 @@ int part_done(Handle<B>* h, const char* what) {
   return h->be.sync() ? fail(std::string(what) + ": " + h->be.error()) : 0;
 }
 
+// the owner side of a round on the received segments: each env's update records in order, then the
+// answer to its request (sfl_part.h part_owner_group)
 template <class B>
-int part_answer(Handle<B>* h, const void* req_in, void* rep_out) {
+int part_owner(Handle<B>* h, const void* msg_in, void* rep_out) {
   SflPart& P = h->part;
-  if (!P.world) return fail("sfl_part_answer: handle not partitioned");
-  h->be.part_answer(h->map, P, (const PartReq*)req_in, (PartRep*)rep_out);
-  return part_done(h, "sfl_part_answer");
-}
-
-template <class B>
-int part_update(Handle<B>* h, const void* upd_in) {
-  SflPart& P = h->part;
-  if (!P.world) return fail("sfl_part_update: handle not partitioned");
-  h->be.part_update_all(h->map, P, (const PartUpd*)upd_in);
-  return part_done(h, "sfl_part_update");
+  if (!P.world) return fail("sfl_part_owner: handle not partitioned");
+  h->be.part_owner(h->map, P, (const PartMsg*)msg_in, (PartRep*)rep_out);
+  return part_done(h, "sfl_part_owner");
 }
 
 // which switches' rows the wave kernel decides on and updates directly: local[S] (null: the
@@ -1075,14 +1064,14 @@ int part_set_local_rows(Handle<B>* h, const uint8_t* local) {
   return h->be.sync() ? fail(h->be.error()) : 0;
 }
 
-// this rank's counts (sfl_part.h PART_C_*): of the last part_local, requests and update records staged
-// per destination and the highest update stage, then the peaks per destination and the deferrals since
-// the previous read, that round's open and deferred envs.  cap >= 2 * world + 1 (the first three only)
+// this rank's counts (sfl_part.h PART_C_*): of the last part_local, message records staged per destination,
+// then their peaks per destination since the previous read, that round's open and deferred envs and the
+// deferrals since the previous read.  cap >= world (the first counts only)
 template <class B>
 int part_counts(Handle<B>* h, uint32_t* out, int32_t cap) {
   if (!h->part.world) return fail("sfl_part_counts: handle not partitioned");
   const int32_t n = PART_NCNT(h->part.world);
-  if (cap < PART_NCNT_LEGACY(h->part.world)) return fail("sfl_part_counts: buffer too small");
+  if (cap < h->part.world) return fail("sfl_part_counts: buffer too small");
   if (h->part_pending)
     if (int rc = part_read(h)) return rc;
   for (int32_t i = 0; i < n && i < cap; ++i) out[i] = i < (int32_t)h->part_counts.size() ? h->part_counts[i] : 0u;

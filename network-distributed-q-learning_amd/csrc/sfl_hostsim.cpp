@@ -95,14 +95,15 @@ struct HostBackend {
     *ms = 0.f;
     return 0;
   }
-  // k_part_compact (sfl.hip) in env order: each env's staged records into the segments (at most k_req /
-  // k_upd per destination; an env with a record past that is deferred whole, its places below the end
-  // get void records), the launch totals of the envs that ran, the headers and the checkpoint counts
+  // k_part_compact (sfl.hip) in env order: each env's staged records into the segments as one group per
+  // destination (sfl_part.h env_groups; at most k_msg records per segment: an env with a group past that is
+  // deferred whole, its places below the end get void records), the launch totals of the envs that ran,
+  // the headers and the checkpoint counts
   static void part_compact(const sfl::SflPart& P, const sfl::SflState& s, const sfl::SflCtl& c) {
     const int W = P.world;
-    const uint32_t kq = P.k_req, ku = P.k_upd;
-    std::vector<uint32_t> nr(W, 0u), nw(W, 0u);
-    uint32_t top = 0, n_open = 0, n_def = 0;
+    const uint32_t k = P.k_msg;
+    std::vector<uint32_t> nm(W, 0u);
+    uint32_t n_open = 0, n_def = 0;
     uint64_t t[4] = {0, 0, 0, 0};
     for (uint32_t e = 0; e < s.E; ++e) {
       const uint32_t flags = s.eflags[e];
@@ -114,34 +115,29 @@ struct HostBackend {
       t[3] |= s.err[e];
       const int rd = P.req_dst[e];
       const uint32_t nu = P.upd_n[e];
-      const sfl::PartUpd* st = P.upd_st + (size_t)e * P.upd_env;
-      const uint32_t kr = rd >= 0 ? nr[rd]++ : 0u;
-      uint32_t ks[sfl::PART_UPD_ENV_MAX];
-      bool fits = rd < 0 || kr < kq;
-      for (uint32_t i = 0; i < nu; ++i) {
-        const int d = P.owner[st[i].port >> 2];
-        ks[i] = nw[d]++;
-        if (ks[i] >= ku) fits = false;
-      }
-      for (uint32_t i = 0; i < nu; ++i) {
-        sfl::PartUpd& u = P.upd_out[(size_t)P.owner[st[i].port >> 2] * (ku + 1) + 1 + ks[i]];
-        if (fits) {
-          u = st[i];
-          top = st[i].stage > top ? st[i].stage : top;
-        } else if (ks[i] < ku) {
-          u.genv = 0u;
-          u.stage = 0;
-          u.kind = sfl::UPD_VOID;
+      int32_t dst[sfl::PART_GROUP_MAX];
+      uint32_t rank[sfl::PART_GROUP_MAX], size[sfl::PART_GROUP_MAX], at[sfl::PART_GROUP_MAX];
+      const uint32_t n = sfl::env_groups(P, e, rd, nu, dst, rank, size);
+      std::vector<uint32_t> gb(W, 0u);
+      for (uint32_t r = 0; r < n; ++r)
+        if (rank[r] == 0) {
+          gb[dst[r]] = nm[dst[r]];
+          nm[dst[r]] += size[r];
         }
+      bool fits = true;
+      for (uint32_t r = 0; r < n; ++r) {
+        at[r] = gb[dst[r]] + rank[r];
+        if (at[r] >= k) fits = false;
       }
-      if (rd >= 0 && (fits || kr < kq)) {
-        sfl::PartReq& r = P.req_out[(size_t)rd * (kq + 1) + 1 + kr];
+      for (uint32_t r = 0; r < n; ++r) {
+        sfl::PartMsg& x = P.msg_out[(size_t)dst[r] * (k + 1) + 1 + at[r]];
         if (fits) {
-          r = P.req_st[e];
-          P.req_ix[e] = (uint32_t)rd * (kq + 1) + 1u + kr;
-        } else {
-          r.genv = 0u;
-          r.flags = sfl::REQ_VOID;
+          x = r < nu ? P.upd_st[(size_t)e * P.upd_env + r] : sfl::msg_of_req(P.req_st[e]);
+          if (rank[r] == 0) x.kind |= size[r] << 8;
+          if (r == nu) P.req_ix[e] = (uint32_t)dst[r] * (k + 1) + 1u + at[r];
+        } else if (at[r] < k) {
+          x.genv = 0u;
+          x.kind = sfl::MSG_VOID | (1u << 8);
         }
       }
       if ((bool)(flags & sfl::F_DEFER) == fits) s.eflags[e] = flags ^ sfl::F_DEFER;
@@ -150,16 +146,10 @@ struct HostBackend {
     }
     uint32_t* co = (uint32_t*)(P.cnt_out + 4);
     for (int g = 0; g < W; ++g) {
-      P.req_out[(size_t)g * (kq + 1)].genv = nr[g] < kq ? nr[g] : kq;
-      sfl::PartUpd& hu = P.upd_out[(size_t)g * (ku + 1)];
-      hu.genv = nw[g] < ku ? nw[g] : ku;
-      hu.state = top;
-      co[sfl::PART_C_REQ(W) + g] = nr[g];
-      co[sfl::PART_C_UPD(W) + g] = nw[g];
-      co[sfl::PART_C_PEAK_REQ(W) + g] = std::max(co[sfl::PART_C_PEAK_REQ(W) + g], nr[g]);
-      co[sfl::PART_C_PEAK_UPD(W) + g] = std::max(co[sfl::PART_C_PEAK_UPD(W) + g], nw[g]);
+      P.msg_out[(size_t)g * (k + 1)].genv = nm[g] < k ? nm[g] : k;
+      co[sfl::PART_C_MSG(W) + g] = nm[g];
+      co[sfl::PART_C_PEAK(W) + g] = std::max(co[sfl::PART_C_PEAK(W) + g], nm[g]);
     }
-    co[sfl::PART_C_STAGE(W)] = top;
     co[sfl::PART_C_OPEN(W)] = n_open;
     co[sfl::PART_C_DEFER(W)] = n_def;
     co[sfl::PART_C_DEFER_SUM(W)] += n_def;
@@ -168,31 +158,20 @@ struct HostBackend {
   }
   int set_stream(void*) { return 0; }  // one host thread: nothing to order
   void part_eblk(const sfl::SflState&, const sfl::SflPart&, int) {}
-  void part_caps(const sfl::SflPart&) {}  // (the host build reads the SflPart itself)  // (the lane body keeps the SflState arrays)
-  void part_answer(const sfl::SflMap& m, const sfl::SflPart& P, const sfl::PartReq* in, sfl::PartRep* out) {
+  void part_caps(const sfl::SflPart&) {}  // (the host build reads the SflPart itself)
+  // k_part_owner: every received group by one thread (the groups are independent: one env's records each)
+  void part_owner(const sfl::SflMap& m, const sfl::SflPart& P, const sfl::PartMsg* in, sfl::PartRep* out) {
     for (int g = 0; g < P.world; ++g) {
-      const size_t base = (size_t)g * (P.k_req + 1);
+      const size_t base = (size_t)g * (P.k_msg + 1);
       const int64_t n = in[base].genv;
 #pragma omp parallel for
-      for (int64_t k = 1; k <= n; ++k)
-        if (in[base + k].flags != sfl::REQ_VOID) sfl::part_answer_one(m, P, in[base + k], out[base + k]);
-    }
-  }
-  // stage by stage up to the highest stage in the received segment headers
-  void part_update_all(const sfl::SflMap& m, const sfl::SflPart& P, const sfl::PartUpd* in) {
-    uint32_t top = 0;
-    for (int g = 0; g < P.world; ++g) {
-      const sfl::PartUpd& hd = in[(size_t)g * (P.k_upd + 1)];
-      if (hd.genv > 0 && hd.state > top) top = hd.state;
-    }
-    for (uint32_t stage = 0; stage <= top; ++stage)
-      for (int g = 0; g < P.world; ++g) {
-        const size_t base = (size_t)g * (P.k_upd + 1);
-        const int64_t n = in[base].genv;
-#pragma omp parallel for
-        for (int64_t k = 1; k <= n; ++k)
-          if (in[base + k].stage == stage) sfl::part_update_one(m, P, in[base + k]);
+      for (int64_t i = 1; i <= n; ++i) {
+        const uint32_t len = sfl::msg_group(in[base + i].kind);
+        if (len == 0u || sfl::msg_type(in[base + i].kind) == sfl::MSG_VOID) continue;
+        sfl::part_owner_group(m, P, in + base + i, len, out + base + i,
+                              [&](const sfl::PartReq& r, sfl::PartRep& rep) { sfl::part_answer_one(m, P, r, rep); });
       }
+    }
   }
 };
 

@@ -10,15 +10,17 @@
 //   local    (env_run_part): apply the reply of the previous round's request, continue the
 //            env (post, ticks, episode ends) up to the next decision, observe it and stage its
 //            request; post steps stage update records
-//   compact  (k_part_compact): the staged records into the destination segments, at most k_req
-//            requests and k_upd update records per segment; an env whose records do not all fit
-//            is deferred whole (F_DEFER: it sends nothing this round and sits out the next local
-//            step, its staged records go again), so the segments have a fixed size and the
+//   compact  (k_part_compact): the staged records into ONE message segment per destination rank,
+//            each env's records for that destination as a contiguous group (its update records in
+//            emission order, then its request); at most k_msg records per segment: an env with a group
+//            that does not fit is deferred whole (F_DEFER: it sends nothing this round and sits out the
+//            next local step, its staged records go again), so the segments have a fixed size and the
 //            exchange needs no counts from the host
-//   exchange updates + requests (RCCL all-to-all; segment per destination rank)
-//   update   (part_update_one): the owner applies the updates, stage by stage
-//   answer   (part_answer_one): the owner computes max(row) and the masked argmax
-//   exchange replies (the same segment layout, back to the requesters)
+//   exchange the message segments (one RCCL all-to-all; segment per destination rank)
+//   owner    (part_owner_group): per received group, the env's updates in order, then the answer to
+//            its request (max(row) and the masked argmax) -- one kernel, no stage ordering across
+//            the segment: an env's records touch only that env's rows, and a group is walked in order
+//   exchange the replies (the same segment layout, back to the requesters)
 // Each env's own sequence of operations is that of env_run (sfl_core.h), so the results are
 // bit-identical to the fused kernels (tests/test_partition.py).
 #pragma once
@@ -28,8 +30,6 @@ namespace sfl {
 
 enum : uint32_t { F_REQ = 64 };     // eflags: a request is waiting for its reply
 enum : uint32_t { F_DEFER = 256 };  // eflags: the env's staged records did not fit this round's segments
-// a record in a segment place left by a deferred env (the owner skips it): PartReq::flags / PartUpd::kind
-constexpr uint32_t REQ_VOID = 2u, UPD_VOID = 2u;
 enum : uint32_t { E_MSG_OVF = 16 };  // a message segment overflowed (capacity too small)
 constexpr uint32_t PART_UPD_ENV_MAX = 16;  // staged update records per env and round, at most
 
@@ -46,14 +46,15 @@ enum : int {
 };
 constexpr int PART_EB = 64;
 
-// message records; record 0 of each destination segment is a header whose first word is the
+// staged records (the env's own slots: its request, its update records) and the 32-byte message
+// record of the segments; record 0 of each destination segment is a header whose first word is the
 // number of records that follow
 struct PartReq {
   uint32_t genv;   // global env index
   uint16_t port;   // 4 * switch + in-port slot (the row's block)
   uint16_t amask;  // allowed actions (get_action_mask)
   uint32_t state;  // observation state index within the block
-  uint32_t flags;  // 1: exploratory action (no argmax, no key-set insert); REQ_VOID: no request
+  uint32_t flags;  // 1: exploratory action (no argmax, no key-set insert)
 };
 struct PartRep {
   int32_t action;  // masked argmax (distr_q.py:468-490); -1 for exploratory requests
@@ -64,13 +65,22 @@ struct PartUpd {
   uint32_t genv;
   uint16_t port;
   uint8_t j;      // compact column
-  uint8_t stage;  // 0: pending update / key-set inserts; 1 + i: bonus of the i-th arrived train
+  uint8_t stage;  // 0: pending update / key-set inserts; 1 + i: bonus of the i-th arrived train (emission order)
   uint32_t state;
-  uint32_t kind;  // 0: q <- (1 - lr) q + lr target;  1: key-set insert only; UPD_VOID: nothing
+  uint32_t kind;  // 0: q <- (1 - lr) q + lr target;  1: key-set insert only
   double lr;
   double target;
 };
+// a segment record (32 B): an update record (MSG_UPD / MSG_INSERT, the PartUpd fields) or a request
+// (MSG_REQ / MSG_REQ_X: genv, port, state as PartReq, amask in `j | stage << 8`).  kind bits 8-15: the
+// length of the env's group when this is its first record (0 inside a group); a deferred env's places
+// below the segment end carry MSG_VOID records of length 1.
+enum : uint32_t { MSG_UPD = 0u, MSG_INSERT = 1u, MSG_VOID = 2u, MSG_REQ = 3u, MSG_REQ_X = 4u };
+typedef PartUpd PartMsg;
+SFL_FN constexpr uint32_t msg_type(uint32_t kind) { return kind & 0xFFu; }
+SFL_FN constexpr uint32_t msg_group(uint32_t kind) { return (kind >> 8) & 0xFFu; }
 static_assert(sizeof(PartReq) == 16 && sizeof(PartRep) == 16 && sizeof(PartUpd) == 32, "record sizes");
+constexpr uint32_t PART_GROUP_MAX = PART_UPD_ENV_MAX + 1;  // records of one env in one segment, at most
 
 struct SflPart {
   int32_t rank, world;
@@ -78,9 +88,10 @@ struct SflPart {
                               // (its owner is this rank; all 0: every row operation as a message)
   uint32_t env_base;  // global index of local env 0
   uint32_t E_tot;     // envs over all ranks
-  uint32_t cap_req, cap_upd;  // records per destination segment (without the header), at most
-  uint32_t k_req, k_upd;      // this round's records per destination segment (<= cap; the segments of
-                              // a buffer are k + 1 records apart): sfl_part_set_caps
+  uint32_t cap_msg;           // records per destination segment (without the header), at most:
+                              // one request and PART_UPD_ENV_MAX update records per env of the largest rank
+  uint32_t k_msg;             // this round's records per destination segment (<= cap_msg; the segments
+                              // of a buffer are k_msg + 1 records apart): sfl_part_set_caps
   uint64_t q_own_per_env;     // doubles of owned Q per env
   uint32_t own_rows, own_words;
   const int32_t* owner;       // [S] rank owning each switch agent
@@ -91,9 +102,8 @@ struct SflPart {
   Obs* obs;                   // [E] observation waiting for its reply
   uint32_t* req_ix;           // [E] record index of that request's reply in the reply buffer
   int64_t* dec_done;          // [E] decisions since sfl_part_begin
-  uint32_t* cnt;              // [2][world] records staged this round (requests, updates; sent or not),
-                              // then max_stage, blocks_done, open envs, deferred envs
-  uint32_t* max_stage;        // [1] highest update stage sent this round
+  uint32_t* cnt;              // [world] message records staged this round (sent or not), then
+                              // blocks_done, open envs, deferred envs
   uint32_t* blocks_done;      // [1] k_part_compact's finished blocks (the last one writes the headers)
   uint64_t* sums;             // [4] this round's launch totals (decisions, ticks, bytes, error bits OR)
   uint64_t* cnt_out;          // [4 + PART_NCNT(world) / 2]: sums, then the counts as u32 (PART_C_*): what the
@@ -106,27 +116,20 @@ struct SflPart {
   PartUpd* upd_st;            // [E][upd_env] the env's update records of this round
   uint32_t* upd_n;            // [E] how many (lane-per-env body)
   uint32_t upd_env;           // staged update records per env and round (E_MSG_OVF beyond)
-  uint32_t* late;             // [1 + world * cap_upd]: count, then the received records of stage >= 1
-                              // (applied in stage order by k_part_update_late)
   uint32_t* eblk;             // [E][PART_EB] the wave kernel's per-env scalars between rounds (null: the
                               // lane-per-env body, which keeps the SflState arrays)
   // round buffers (set per call)
-  const PartRep* rep_in;      // [world][k_req + 1]
-  PartReq* req_out;           // [world][k_req + 1]
-  PartUpd* upd_out;           // [world][k_upd + 1]
+  const PartRep* rep_in;      // [world][k_msg + 1] (a reply sits at its request's record index)
+  PartMsg* msg_out;           // [world][k_msg + 1]
 };
 
 // the counts a checkpoint reads (sfl_part_counts), u32 words after the four launch totals of cnt_out
-SFL_FN constexpr int PART_C_REQ(int) { return 0; }                     // [world] requests staged this round
-SFL_FN constexpr int PART_C_UPD(int w) { return w; }                   // [world] update records staged
-SFL_FN constexpr int PART_C_STAGE(int w) { return 2 * w; }             // highest update stage
-SFL_FN constexpr int PART_C_PEAK_REQ(int w) { return 2 * w + 1; }      // [world] peak of C_REQ since the read
-SFL_FN constexpr int PART_C_PEAK_UPD(int w) { return 3 * w + 1; }      // [world] peak of C_UPD since the read
-SFL_FN constexpr int PART_C_OPEN(int w) { return 4 * w + 1; }          // envs with a request or deferred
-SFL_FN constexpr int PART_C_DEFER(int w) { return 4 * w + 2; }         // envs deferred this round
-SFL_FN constexpr int PART_C_DEFER_SUM(int w) { return 4 * w + 3; }     // deferrals since the read
-SFL_FN constexpr int PART_NCNT(int w) { return 4 * w + 4; }
-SFL_FN constexpr int PART_NCNT_LEGACY(int w) { return 2 * w + 1; }   // (the round-3 count vector: its prefix)
+SFL_FN constexpr int PART_C_MSG(int) { return 0; }                    // [world] message records staged this round
+SFL_FN constexpr int PART_C_PEAK(int w) { return w; }                 // [world] peak of C_MSG since the read
+SFL_FN constexpr int PART_C_OPEN(int w) { return 2 * w; }             // envs with a request or deferred
+SFL_FN constexpr int PART_C_DEFER(int w) { return 2 * w + 1; }        // envs deferred this round
+SFL_FN constexpr int PART_C_DEFER_SUM(int w) { return 2 * w + 2; }    // deferrals since the read
+SFL_FN constexpr int PART_NCNT(int w) { return 2 * w + 3; }
 
 SFL_FN void fetch_or_u32(uint32_t* p, uint32_t v) {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -171,6 +174,29 @@ struct MapView {
   const SflMap& m;
 };
 
+// a request as a segment record and back (sfl_part.h PartMsg: amask in j | stage << 8)
+SFL_FN PartMsg msg_of_req(const PartReq& r) {
+  PartMsg x;
+  x.genv = r.genv;
+  x.port = r.port;
+  x.j = (uint8_t)(r.amask & 0xFFu);
+  x.stage = (uint8_t)(r.amask >> 8);
+  x.state = r.state;
+  x.kind = (r.flags & 1u) ? MSG_REQ_X : MSG_REQ;
+  x.lr = 0.0;
+  x.target = 0.0;
+  return x;
+}
+SFL_FN PartReq req_of_msg(const PartMsg& x) {
+  PartReq r;
+  r.genv = x.genv;
+  r.port = x.port;
+  r.amask = (uint16_t)(x.j | ((uint32_t)x.stage << 8));
+  r.state = x.state;
+  r.flags = msg_type(x.kind) == MSG_REQ_X ? 1u : 0u;
+  return r;
+}
+
 // owner side: one request -> reply (distr_q.py:449-490 on the owned row)
 SFL_FN void part_answer_one(const SflMap& m, const SflPart& P, const PartReq& r, PartRep& out) {
   const int port = r.port, sw = port >> 2, slot = port & 3;
@@ -178,7 +204,7 @@ SFL_FN void part_answer_one(const SflMap& m, const SflPart& P, const PartReq& r,
   const MapView mv{m};
   out.mq = row_max(mv, sw, slot, row);
   out.pad = 0;
-  if (r.flags & 1u) {  // (REQ_VOID records are skipped by the callers)
+  if (r.flags & 1u) {
     out.action = -1;
   } else {
     const uint32_t rid = P.row_own[port] + r.state;
@@ -187,18 +213,57 @@ SFL_FN void part_answer_one(const SflMap& m, const SflPart& P, const PartReq& r,
   }
 }
 
-// owner side: one update record of the given stage
+// owner side: one update record (MSG_UPD: the bootstrapped update and the key-set insert; MSG_INSERT: the
+// insert only)
 SFL_FN void part_update_one(const SflMap& m, const SflPart& P, const PartUpd& u) {
-  if (u.kind == UPD_VOID) return;
   const int port = u.port;
   const uint32_t rid = P.row_own[port] + u.state;
   fetch_or_u32(&P.touched_own[(size_t)u.genv * P.own_words + (rid >> 5)], 1u << (rid & 31u));
-  if (u.kind == 0u) {
+  if (msg_type(u.kind) == MSG_UPD) {
     double* q = P.q_own + (size_t)u.genv * P.q_own_per_env + P.q_off_own[port] + (size_t)u.state * m.q_w[port] + u.j;
     const double a = (1.0 - u.lr) * *q;
     const double bb = u.lr * u.target;
     *q = a + bb;
   }
+}
+
+// owner side: one env's group of a received segment, in order -- its update records as the env emitted
+// them (the pending update, key-set inserts, arrival bonuses: distr_q.py:325-362), then the answer to its
+// request, which may read a row those updates just wrote.  An env's records touch only that env's rows
+// (q_own / touched_own of its genv), so groups are independent of each other.
+template <class Answer>
+SFL_FN void part_owner_group(const SflMap& m, const SflPart& P, const PartMsg* g, uint32_t len, PartRep* rep,
+                             Answer&& answer) {
+  for (uint32_t i = 0; i < len; ++i) {
+    const uint32_t t = msg_type(g[i].kind);
+    if (t == MSG_UPD || t == MSG_INSERT) part_update_one(m, P, g[i]);
+    else if (t == MSG_REQ || t == MSG_REQ_X) answer(req_of_msg(g[i]), rep[i]);
+  }
+}
+
+// sender side: an env's staged records grouped per destination (k_part_compact, the host build's
+// part_compact).  Record r < nu is update r, to the owner of its row's switch; record nu the request, to rd
+// (if rd >= 0); dst = -1 past the last.  rank[r]: the record's place in its destination's group (emission
+// order, so the request comes last); size[r]: that group's length.  Returns the number of records.
+SFL_FN uint32_t env_groups(const SflPart& P, uint32_t e, int rd, uint32_t nu, int32_t (&dst)[PART_GROUP_MAX],
+                           uint32_t (&rank)[PART_GROUP_MAX], uint32_t (&size)[PART_GROUP_MAX]) {
+  const uint32_t n = nu + (rd >= 0 ? 1u : 0u);
+#pragma unroll
+  for (uint32_t r = 0; r < PART_GROUP_MAX; ++r)
+    dst[r] = r < nu ? P.owner[P.upd_st[(size_t)e * P.upd_env + r].port >> 2] : (r == nu && rd >= 0) ? rd : -1;
+#pragma unroll
+  for (uint32_t r = 0; r < PART_GROUP_MAX; ++r) {
+    uint32_t k = 0, z = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < PART_GROUP_MAX; ++q) {
+      const bool same = q < n && dst[q] == dst[r];
+      k += (same && q < r) ? 1u : 0u;
+      z += same ? 1u : 0u;
+    }
+    rank[r] = k;
+    size[r] = z;
+  }
+  return n;
 }
 
 // local side: one env for one round (env_run of sfl_core.h, with the Q row operations sent to

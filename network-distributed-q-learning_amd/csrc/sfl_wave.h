@@ -867,7 +867,7 @@ struct WEnv {
       {  // the reply, if a request is open (a stale index of an env without one stays inside the buffer)
         const uint32_t ix = U(ixr);
         const vec_t<int32_t, 4> rw =
-            ld((const vec_t<int32_t, 4>*)(P->rep_in + (ix < P->world * (P->cap_req + 1u) ? ix : 0u)), 0);
+            ld((const vec_t<int32_t, 4>*)(P->rep_in + (ix < P->world * (P->cap_msg + 1u) ? ix : 0u)), 0);
         rep_a = (uint32_t)rw[0];
         rep_lo = (uint32_t)rw[2];
         rep_hi = (uint32_t)rw[3];

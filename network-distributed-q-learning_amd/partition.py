@@ -8,17 +8,18 @@ its switches for every env of the job and answers the row lookups for them; envs
 over the ranks as in the env-sharded mode.  Each round every env makes one decision:
 
     sfl_part_local    apply last round's reply, run to the next decision, emit its request
-                      (and the update records of the post step)
-    all-to-all        update + request buffers  (RCCL over xGMI: torch.distributed "nccl")
-    sfl_part_update   owner applies the bootstrapped updates (stage-ordered)
-    sfl_part_answer   owner: max over the row + masked argmax
+                      (and the update records of the post step), packed per destination rank
+                      with each env's records as one contiguous group
+    all-to-all        the message segments  (RCCL over xGMI: torch.distributed "nccl")
+    sfl_part_owner    owner, per env group: the bootstrapped updates in order, then max over
+                      the requested row + masked argmax
     all-to-all        replies back
 
-Every env performs exactly the operations of the fused kernels in the same order, so the
-results are bit-identical to the single-process run (tests/test_partition.py).  Message
-buffers are [world][k + 1] record segments whose first record carries the count; an env whose
-records do not fit a segment is deferred whole to a later round (k_part_compact), so each
-exchange is a fixed-size all-to-all.  On the GPU the rounds queue on one stream (this batch's
+Two collectives per round.  Every env performs exactly the operations of the fused kernels in
+the same order, so the results are bit-identical to the single-process run
+(tests/test_partition.py).  Message buffers are [world][k + 1] record segments whose first
+record carries the count; an env whose group does not fit a segment is deferred whole to a later
+round (k_part_compact), so each exchange is a fixed-size all-to-all.  On the GPU the rounds queue on one stream (this batch's
 torch stream, handed to the library with sfl_set_stream; RCCL collectives follow it): the host
 reads the counts only at checkpoint rounds (1, 2, 4, ..., 32, then every 32nd), where the ranks
 also agree on the next segment sizes -- no host synchronisation in the rounds between.
@@ -82,7 +83,7 @@ class PartitionedBatch:
                  rank: int = 0, world: int = 1, dist=None, lib: Optional[_lib.Lib] = None, device: int = 0,
                  owner: Optional[np.ndarray] = None, upd_per_env: int = 16, ntab: Optional[int] = None,
                  buffer_device: str = "cuda", local_rows=True, malfunction_stream: str = "counter",
-                 delay_threshold: int = 20, k_init: Optional[tuple] = None):
+                 delay_threshold: int = 20, k_init: Optional[int] = None, checkpoint_every_round: bool = False):
         import torch
         self.torch = torch
         kw = {} if ntab is None else dict(ntab=ntab)
@@ -106,33 +107,35 @@ class PartitionedBatch:
         self.lib.check(self.lib.dll.sfl_part_config(self.batch.h, self.rank, self.world, _ptr(self.owner, C.c_int32),
                                                     self.env_base, self.envs_total, self.cap_req, self.cap_upd),
                        "sfl_part_config")
-        rq, rp, up = C.c_uint32(), C.c_uint32(), C.c_uint32()
-        self.lib.dll.sfl_part_record_sizes(C.byref(rq), C.byref(rp), C.byref(up))
+        ms, rp = C.c_uint32(), C.c_uint32()
+        self.lib.check(self.lib.dll.sfl_part_record_sizes(C.byref(ms), C.byref(rp)), "sfl_part_record_sizes")
+        # one segment per destination holds every env group of the largest rank: its requests and updates
+        self.cap_msg = self.cap_req + self.cap_upd
         dev = torch.device(buffer_device)
-        nreq = self.world * (self.cap_req + 1) * rq.value
-        nrep = self.world * (self.cap_req + 1) * rp.value
-        nupd = self.world * (self.cap_upd + 1) * up.value
+        nmsg = self.world * (self.cap_msg + 1) * ms.value
+        nrep = self.world * (self.cap_msg + 1) * rp.value
         z = lambda n: torch.zeros(n, dtype=torch.uint8, device=dev)  # noqa: E731
         if self.world == 1:
             # one rank: every segment is addressed to this rank, so the exchange is the identity
             # and each receive buffer is its send buffer (no copies, no stream synchronisation)
-            self.req_send = self.req_recv = z(nreq)
+            self.msg_send = self.msg_recv = z(nmsg)
             self.rep_send = self.rep_recv = z(nrep)
-            self.upd_send = self.upd_recv = z(nupd)
         else:
-            self.req_send, self.req_recv = z(nreq), z(nreq)
+            self.msg_send, self.msg_recv = z(nmsg), z(nmsg)
             self.rep_send, self.rep_recv = z(nrep), z(nrep)
-            self.upd_send, self.upd_recv = z(nupd), z(nupd)
         self.on_gpu = dev.type == "cuda"
-        self.rec = (rq.value, rp.value, up.value)
+        self.rec = (ms.value, rp.value)
         self.rounds = 0
-        self._counts = (C.c_uint32 * (4 * self.world + 4))()   # sfl_part_counts, sfl_part.h PART_C_*
-        self.k_req, self.k_upd = self.cap_req, self.cap_upd
+        self._counts = (C.c_uint32 * (2 * self.world + 3))()   # sfl_part_counts, sfl_part.h PART_C_*
+        self.k_msg = self.cap_msg
         self.host_reads = 0   # checkpoint reads of the counts (the host's only look at a round's results)
         self.checkpoints = 0
         self.deferrals = 0    # envs deferred by a full segment, summed over rounds
+        # (tests) read the counts after every round, so that an error surfaces in the round that set it
+        self.checkpoint_every_round = bool(checkpoint_every_round)
+        self.error_round = None  # the round (within its step) at which the last step raised
         if k_init is not None:  # (tests: start below the demand, so that envs are deferred)
-            self.set_caps(*k_init)
+            self.set_caps(k_init)
         # rows of this rank's own switches are decided on / updated in place (no message to itself).
         # local_rows: True (all own switches), False (every row operation as a message: the message
         # path measured on one rank) or a [S] mask of own switches (e.g. one block of a bigger job's
@@ -188,19 +191,19 @@ class PartitionedBatch:
     def apply_qinit(self):
         self.batch.apply_qinit()
 
-    # ---- segment capacities ---------------------------------------------------------------------
-    # A round's buffers are [world][k + 1] records: k_req requests and k_upd update records per
-    # destination.  An env whose records do not all fit is deferred whole by k_part_compact (it
-    # sends nothing that round, sits out the next local step and sends the same records again),
-    # so results never depend on k.  At a checkpoint the ranks agree (one MAX all-reduce) on k from
-    # the peak per-destination demand since the previous checkpoint: every round in between is a
-    # fixed-size all-to-all that needs no counts from the host.  One rank keeps the full capacities
-    # (its exchange is the identity: nothing to save, nothing to defer).
-    def set_caps(self, k_req: int, k_upd: int):
-        k_req, k_upd = int(k_req), int(k_upd)
-        if (k_req, k_upd) != (self.k_req, self.k_upd):
-            self.lib.check(self.lib.dll.sfl_part_set_caps(self.batch.h, k_req, k_upd), "sfl_part_set_caps")
-            self.k_req, self.k_upd = k_req, k_upd
+    # ---- segment capacity ------------------------------------------------------------------------
+    # A round's buffers are [world][k + 1] records: k message records (requests and update records)
+    # per destination.  An env whose group does not fit is deferred whole by k_part_compact (it sends
+    # nothing that round, sits out the next local step and sends the same records again), so results
+    # never depend on k.  At a checkpoint the ranks agree (one MAX all-reduce) on k from the peak
+    # per-destination demand since the previous checkpoint: every round in between is a fixed-size
+    # all-to-all that needs no counts from the host.  One rank keeps the full capacity (its exchange
+    # is the identity: nothing to save, nothing to defer).
+    def set_caps(self, k_msg: int):
+        k_msg = int(k_msg)
+        if k_msg != self.k_msg:
+            self.lib.check(self.lib.dll.sfl_part_set_caps(self.batch.h, k_msg), "sfl_part_set_caps")
+            self.k_msg = k_msg
 
     @staticmethod
     def _resize(k: int, peak: int, cap: int) -> int:
@@ -249,8 +252,10 @@ class PartitionedBatch:
 
     def _checkpoint(self, r: int, last: int) -> bool:
         """Rounds after which the host reads the counts: 1, 2, 4, ..., 32, every 32nd, the round a step
-        without deferrals ends at (decisions + 1), and every 8th after it."""
-        return (r & (r - 1) == 0 and r <= 32) or r % 32 == 0 or r == last or (r > last and (r - last) % 8 == 0)
+        without deferrals ends at (decisions + 1), and every 8th after it (every round with
+        checkpoint_every_round)."""
+        return (self.checkpoint_every_round or (r & (r - 1) == 0 and r <= 32) or r % 32 == 0 or r == last
+                or (r > last and (r - last) % 8 == 0))
 
     def _step(self, decisions_per_env: int) -> int:
         d = self.lib.dll
@@ -258,49 +263,49 @@ class PartitionedBatch:
         W = self.world
         ptr = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
         self.lib.check(d.sfl_part_begin(h), "sfl_part_begin")
-        rq, rp, up = self.rec
+        ms, rp = self.rec
         last = int(decisions_per_env) + 1
         limit = 4 * last + 64  # (deferrals add rounds; each checkpoint resizes the segments to the demand)
         rounds, failed, msg = 0, False, ""
+        self.error_round = None
+
+        def fail(what):
+            # a failure on this rank (a launch error) must not leave the others waiting in the next
+            # exchange: it sends empty segments until the checkpoint, where every rank stops
+            nonlocal failed, msg
+            failed, msg = True, what + ": " + d.sfl_last_error().decode(errors="replace")
         while True:
             rounds += 1
-            if not failed:
-                # a failure on this rank (a launch error) must not leave the others waiting in the next
-                # exchange: it sends empty segments until the checkpoint, where every rank stops
-                rc = d.sfl_part_local(h, int(decisions_per_env), ptr(self.rep_recv), ptr(self.req_send),
-                                      ptr(self.upd_send), None)
-                if rc:
-                    failed, msg = True, d.sfl_last_error().decode(errors="replace")
+            if not failed and d.sfl_part_local(h, int(decisions_per_env), ptr(self.rep_recv), ptr(self.msg_send), None):
+                fail("sfl_part_local")
             if failed and W > 1:
-                self._view(self.req_send, self.k_req, rq).view(W, -1)[:, :rq].zero_()
-                self._view(self.upd_send, self.k_upd, up).view(W, -1)[:, :up].zero_()
-                self._view(self.rep_send, self.k_req, rp).zero_()
-            self._a2a(self.upd_recv, self.upd_send, self.k_upd, up)
-            self._a2a(self.req_recv, self.req_send, self.k_req, rq)
-            if not failed:
-                self.lib.check(d.sfl_part_update(h, ptr(self.upd_recv)), "sfl_part_update")
-                self.lib.check(d.sfl_part_answer(h, ptr(self.req_recv), ptr(self.rep_send)), "sfl_part_answer")
-            self._a2a(self.rep_recv, self.rep_send, self.k_req, rp)
+                self._view(self.msg_send, self.k_msg, ms).view(W, -1)[:, :ms].zero_()
+            self._a2a(self.msg_recv, self.msg_send, self.k_msg, ms)
+            if not failed and d.sfl_part_owner(h, ptr(self.msg_recv), ptr(self.rep_send)):
+                fail("sfl_part_owner")
+            if failed and W > 1:
+                self._view(self.rep_send, self.k_msg, rp).zero_()
+            self._a2a(self.rep_recv, self.rep_send, self.k_msg, rp)
             if not self._checkpoint(rounds, last) and rounds < limit:
                 continue
             self.checkpoints += 1
             c = None if failed else self._read_counts()
             if c is None and not msg:
-                msg = d.sfl_last_error().decode(errors="replace")
+                msg = "sfl_part_local: " + d.sfl_last_error().decode(errors="replace")
             err = 1 if c is None else 0
             c = c or [0] * len(self._counts)
-            self.deferrals += c[4 * W + 3]
-            job = self._all_max([err, c[4 * W + 1], max(c[2 * W + 1:3 * W + 1]), max(c[3 * W + 1:4 * W + 1])])
+            self.deferrals += c[2 * W + 2]
+            job = self._all_max([err, c[2 * W], max(c[W:2 * W])])
             if job[0]:
-                raise _lib.SflError(f"rank {self.rank}: sfl_part_local: " + (msg or "stopped because another rank failed"))
+                self.error_round = rounds
+                raise _lib.SflError(f"rank {self.rank}: " + (msg or "stopped because another rank failed"))
             if job[1] == 0:
                 break  # every env has made its decisions (this round's updates are applied)
             if rounds >= limit:
                 raise _lib.SflError(f"rank {self.rank}: requests still open after {rounds} rounds "
-                                    f"({c[4 * W + 1]} envs on this rank)")
+                                    f"({c[2 * W]} envs on this rank)")
             if W > 1:
-                self.set_caps(self._resize(self.k_req, job[2], self.cap_req),
-                              self._resize(self.k_upd, job[3], self.cap_upd))
+                self.set_caps(self._resize(self.k_msg, job[2], self.cap_msg))
         self.rounds += rounds
         return rounds
 

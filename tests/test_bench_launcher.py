@@ -40,8 +40,28 @@ def test_gpus_2_launches_two_ranks_end_to_end():
     assert res["config"]["parallelism"] == "env-batch dp2"
     assert res["parity"] == "ok" and res["parity_envs_checked"] == 4, res
     assert "rehearsal" in res and res["roofline"] is None
+    assert res["partition_leg"]["parity"] == "ok" and res["partition_leg"]["world_size"] == 2
     # every rank's decisions are in the job's total: 2 ranks x 4 envs x 32 decisions x 2 timed steps
     assert abs(res["value"] * res["ms_per_step"] * 1e-3 * res["steps"] - 2 * 4 * 32 * 2) < 1e-6 * res["value"] + 1
+
+
+def test_gpus_4_host_rehearsal_runs_the_partitioned_leg():
+    """The driver's SCALE runs (--gpus N > 1) carry configs[4]'s partitioned leg on the same ranks.  Rehearsed
+    here on four host-build ranks over gloo end to end: the env-sharded line plus the leg, whose owned Q rows and
+    env states are checked against a fused host run (parity ok), with one message exchange and one reply
+    exchange per round."""
+    r = _bench(["--gpus", "4", "--rehearse-on-host", "--config", "c2", "--envs", "4", "--decisions", "32",
+                "--steps", "2", "--warmup", "1", "--verify-envs", "2"], _env(OMP_NUM_THREADS="2"), timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    res = json.loads(lines[0])
+    assert res["world_size"] == 4 and res["parity"] == "ok"
+    leg = res["partition_leg"]
+    assert "error" not in leg, leg
+    assert leg["world_size"] == 4 and leg["backend"] == "gloo" and leg["parity"] == "ok", leg
+    assert leg["parity_envs_checked"] == 8 and leg["collectives_per_round"] == 2 and "rehearsal" in leg
+    assert leg["rounds_per_step"] >= 25  # (the host build's local step sends every row: decisions + 1 rounds)
 
 
 def test_world_size_other_than_gpus_is_refused():

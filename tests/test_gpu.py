@@ -243,37 +243,26 @@ def test_partitioned_rounds_gpu_equal_fused(lib, cfg, E, kernel, local_rows):
     ref.close()
 
 
-def test_partition_staging_overflow_raised(lib):
+def test_partition_staging_overflow_reported_in_its_step(lib):
     """More update records in one env's round than its staging slots hold (upd_per_env 2, every row a
-    message): the GPU run raises E_MSG_OVF (flag 16) at the end of the step where it happened, like the
-    host build.  (Segments themselves no longer overflow: an env that does not fit is deferred, round 4.
-    The two bodies stage different numbers of key-set inserts -- the lane body sends one where k_wave's
-    owner inserts while answering -- so the step at which each overflows can differ.)"""
-    from tests import hostsim
+    message): the wave kernel's run raises E_MSG_OVF (flag 16) in the step where it happened -- the same step
+    as the same GPU kernel reading its counts after every round (which pins the round that set it), at the
+    first checkpoint round at or after that round.  (The host build is not the comparison here: the lane body
+    stages one key-set insert where k_wave's owner inserts while answering, so they overflow at different
+    steps; tests/test_partition.py checks the same property on the host build.)"""
+    from tests import test_partition
     part = importlib.import_module("network-distributed-q-learning_amd.partition")
-    _lib = importlib.import_module("network-distributed-q-learning_amd._lib")
     cm = comp.compile_scenario(mapgen.make_config("c2"))
     seeds = [3000 + i for i in range(64)]
-
-    def first_failing_step(pb):
-        pb.learn_begin()
-        pb.apply_qinit()
-        for i in range(40):
-            try:
-                pb.step(3)
-            except _lib.SflError as ex:
-                assert "error flags 0x10" in str(ex) or "segment overflow" in str(ex), str(ex)
-                return i
-        return None
-
-    kw = dict(ntab=1 << 14, local_rows=False, upd_per_env=2)
-    gpu_pb = part.PartitionedBatch(cm, HP, seeds, 0, len(seeds), lib=lib, buffer_device="cuda", **kw)
-    assert gpu_pb.cap_upd == 128 and gpu_pb.batch.counters()["kernel_variant"] > 0
-    host_pb = part.PartitionedBatch(cm, HP, seeds, 0, len(seeds), lib=hostsim.lib(), buffer_device="cpu", **kw)
-    i_gpu, i_host = first_failing_step(gpu_pb), first_failing_step(host_pb)
-    gpu_pb.close()
-    host_pb.close()
-    assert i_host is not None and i_gpu is not None
+    kw = dict(lib=lib, buffer_device="cuda", ntab=1 << 14, local_rows=False, upd_per_env=2)
+    every = part.PartitionedBatch(cm, HP, seeds, 0, len(seeds), checkpoint_every_round=True, **kw)
+    dflt = part.PartitionedBatch(cm, HP, seeds, 0, len(seeds), **kw)
+    assert dflt.cap_upd == 128 and dflt.batch.counters()["kernel_variant"] > 0
+    (i_e, r_e), (i_d, r_d) = test_partition._first_failing_step(every), test_partition._first_failing_step(dflt)
+    every.close()
+    dflt.close()
+    assert i_e is not None and i_d == i_e, (i_e, i_d)
+    assert r_d == min(r for r in range(r_e, 4 * 4 + 65) if dflt._checkpoint(r, 4)), (r_e, r_d)
 
 
 @pytest.mark.parametrize("cfg,world", [("c2", 2), ("c5", 2), ("c5", 3)])
@@ -298,10 +287,10 @@ def test_two_rank_partition_gpu_rounds_queue_between_checkpoints(lib):
 
 
 def test_two_rank_partition_gpu_deferred_envs_bit_equal(lib):
-    """k_part_compact's deferral on the device: segments of 1 request / 2 update records per destination to
-    start with, envs deferred whole and skipped by the wave kernel's local step until they fit."""
+    """k_part_compact's deferral on the device: segments of 2 message records per destination to start with,
+    envs deferred whole and skipped by the wave kernel's local step until they fit."""
     from tests import test_partition
-    stats = test_partition.two_rank_run("c5", gpu=True, world=2, steps=(90, 60), k_init=(1, 2))
+    stats = test_partition.two_rank_run("c5", gpu=True, world=2, steps=(90, 60), k_init=2)
     assert sum(st["deferrals"] for st in stats) > 0
 
 
