@@ -98,14 +98,15 @@ def cpu_baseline(cm, seconds: float, config: str = "c3"):
                        f"after one untimed 64-decision step")
 
 
-def cpu_oracle_baseline(sc, seconds: float, check=None):
-    """Second data point: the CPU oracle (pure-Python restatement of the reference loop, the
-    reference's own speed class), one env, one core.  check = (cm, device, group_lanes): afterwards the
-    product kernel runs the same env (seed, map, hyper-parameters) for the same decisions at the bench's
-    group size, and its Q-table must equal the oracle's (the reference's q_table dict) -- the bench line's
-    own oracle parity on exactly the sample it timed."""
+def _oracle_worker(job):
+    """One host core of the oracle baseline: the oracle's learn loop on one env (seed) for about `seconds`,
+    in chunks of 100 decisions.  Runs in a process started before this job touched the GPU."""
+    config, seed, seconds, want_q = job
+    sys.path.insert(0, REPO)
     from oracle import sfl_oracle as so
-    env, model = so.build(sc, 450565, HP, trace=False)
+    mapgen = importlib.import_module(PKG + ".mapgen")
+    sc = mapgen.make_config(config)
+    env, model = so.build(sc, seed, HP, trace=False)
     state = None
     n = 0
     t0 = time.perf_counter()
@@ -113,9 +114,41 @@ def cpu_oracle_baseline(sc, seconds: float, check=None):
         n += 100
         state = so.run_decisions(model, n, state)
     dt = time.perf_counter() - t0
-    out = dict(value=n / dt, unit="agent-env-steps/sec", cores=1, kind="port",
-               sample=f"oracle/sfl_oracle.py learn loop, 1 env of the {sc.name if hasattr(sc, 'name') else 'bench'} "
-                      f"map, {n} decisions in {dt:.1f} s (from episode start, incl. the Q-table init)")
+    return n, dt, (dict(model.q) if want_q else None)
+
+
+def oracle_cores() -> int:
+    """Host cores the oracle baseline runs on: the cgroup CPU quota (the GPU box grants 16) or the affinity set."""
+    cores, quota = host_cores()
+    return max(1, min(cores, int(quota)) if quota else cores)
+
+
+def start_oracle_pool(n: int):
+    """The oracle baseline's worker processes, started BEFORE any HIP call of this process (a process that has
+    initialised the GPU must not start programs: spawn = fork + exec)."""
+    import multiprocessing as mp
+    return mp.get_context("spawn").Pool(n)
+
+
+def cpu_oracle_baseline(config: str, seconds: float, pool=None, check=None):
+    """The reference-speed CPU baseline: the CPU oracle (pure-Python restatement of the reference loop,
+    the reference's own speed class) as one process per granted host core, one env each -- the analogue of
+    the reference's scale-out, one process per seed (hyperparam_tuning.py:85-91).  value = decisions of all
+    processes / the longest process time.  check = (cm, device, group_lanes): afterwards the product kernel runs
+    process 0's env (seed, map, hyper-parameters) for the same decisions at the bench's group size, and its
+    Q-table must equal the oracle's (the reference's q_table dict) -- the bench line's own oracle parity on
+    exactly the sample it timed."""
+    jobs = [(config, 450565 + i, seconds, i == 0) for i in range(pool._processes if pool is not None else 1)]
+    res = pool.map(_oracle_worker, jobs) if pool is not None else [_oracle_worker(jobs[0])]
+    n_all = sum(r[0] for r in res)
+    dt_max = max(r[1] for r in res)
+    n0, dt0, q0 = res[0]
+    out = dict(value=n_all / dt_max, unit="agent-env-steps/sec", cores=len(res), kind="port",
+               sample=f"oracle/sfl_oracle.py learn loop, {len(res)} process(es) (one per granted host core), one env "
+                      f"each (seeds 450565+i) of the {config} map, {n_all} decisions in {dt_max:.1f} s (from episode "
+                      f"start, incl. the Q-table init); 1 core: {n0 / dt0:.4g} agent-env-steps/s ({n0} decisions in "
+                      f"{dt0:.1f} s)",
+               one_core_value=n0 / dt0)
     if check is not None:
         cm, device, g = check
         runtime = importlib.import_module(PKG + ".runtime")
@@ -131,14 +164,14 @@ def cpu_oracle_baseline(sc, seconds: float, check=None):
         try:
             b.learn_begin()
             b.apply_qinit()
-            b.step(n)
+            b.step(n0)
             c = b.counters()
-            same = b.q_dict(0) == model.q
+            same = b.q_dict(0) == q0
             out["oracle_parity"] = {
                 "result": "ok" if same else "FAIL",
                 "what": f"the product kernel (k_wave variant {c['kernel_variant']}, {c['group_lanes']} lanes per env) on "
-                        f"the same env for the same {n} decisions: Q-table (the reference's q_table dict) equal to "
-                        "the oracle's" + ("" if same else " -- it is not")}
+                        f"process 0's env for the same {n0} decisions: Q-table (the reference's q_table dict) equal "
+                        "to the oracle's" + ("" if same else " -- it is not")}
         finally:
             b.close()
     return out
@@ -331,6 +364,10 @@ def main():
     host = args.rehearse_on_host
     par = importlib.import_module(PKG + ".parallel")
     world, rank, local = par.world()
+    pool = None
+    if world == 1 and not args.no_cpu and not host and not any(k.startswith("ROCPROF") for k in os.environ):
+        # (before the first HIP call; never under rocprofv3, whose preload initialises the GPU at start)
+        pool = start_oracle_pool(oracle_cores())
     dist, dev, red_dev = dist_setup(par, local, host)
     if not host:
         torch.cuda.set_device(dev)
@@ -434,8 +471,11 @@ def main():
             res["roofline"] = None
         if world == 1 and not args.no_cpu and not host:
             res["cpu_baseline"] = cpu_baseline(cm, args.cpu_seconds, args.config)
-            res["cpu_oracle_baseline"] = cpu_oracle_baseline(sc, args.cpu_seconds / 2,
+            res["cpu_oracle_baseline"] = cpu_oracle_baseline(args.config, args.cpu_seconds / 2, pool=pool,
                                                              check=(cm, dev, cnt0["group_lanes"]))
+    if pool is not None:
+        pool.close()
+        pool.join()
     b.close()
     printed = []
 
@@ -582,13 +622,14 @@ def partition_run(args, par, dist, world, rank, dev, red_dev, devices, host: boo
 
 # configs[4] inside every N > 1 run of the default bench: the driver launches bench.py itself under
 # torch.distributed.run, so this is where the partitioned exchange meets RCCL on a multi-GPU node.  A short run
-# (c5, 2,048 envs per GPU, 64 decisions per step), after the env-sharded measurement, parity-checked like
+# (c5, 2,048 envs per GPU, 4 timed steps of 256 decisions after 2 warm-up steps, 8 envs of the job re-run on
+# the host build), after the env-sharded measurement, parity-checked like
 # --partition.  A failure of the leg must not cost the bench line, and must not look like success either: rank 0
 # prints the line with the leg's error and every rank exits with PARTITION_LEG_FAILED -- on an exception at once
 # (rank 0) or after the watchdog (the other ranks wait for it, so that the launcher does not stop rank 0 before it
 # has printed), on a hang by the watchdog (rank 0 first).  SFL_NO_PARTITION_LEG=1 skips it.  --rehearse-on-host
 # runs it on the host build (PARTITION_LEG_HOST).
-PARTITION_LEG = dict(config="c5", envs=2048, decisions=64, steps=2, warmup=1, verify_envs=2, remote_rows=False,
+PARTITION_LEG = dict(config="c5", envs=2048, decisions=256, steps=4, warmup=2, verify_envs=8, remote_rows=False,
                      virtual_ranks=0)
 PARTITION_LEG_HOST = dict(PARTITION_LEG, envs=4, decisions=24, steps=1)
 PARTITION_LEG_TIMEOUT_S = 300.0

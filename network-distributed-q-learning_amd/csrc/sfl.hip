@@ -120,7 +120,7 @@ __global__ void __launch_bounds__(64) k_part_compact(const sfl::SflPart* __restr
   int rd = -1;
   uint32_t nu = 0, flags = 0, n = 0;
   int32_t dst[R];
-  uint32_t rank[R], size[R], place[R];
+  uint32_t pos[R], size[R], place[R];
   // the wave kernel's per-env words (its scalar block, sfl_part.h EB_*), or the lane kernel's arrays
   const uint32_t* eb = (valid && !arrays) ? P->eblk + (size_t)e * sfl::PART_EB : nullptr;
   auto eb64 = [&](int i) { return (unsigned long long)eb[i] | ((unsigned long long)eb[i + 1] << 32); };
@@ -128,18 +128,9 @@ __global__ void __launch_bounds__(64) k_part_compact(const sfl::SflPart* __restr
     flags = eb ? eb[sfl::EB_EFLAGS] : s->eflags[e];
     rd = eb ? (int)eb[sfl::EB_REQ_DST] : P->req_dst[e];
     nu = eb ? eb[sfl::EB_UPD_N] : P->upd_n[e];
-    n = sfl::env_groups(*P, e, rd, nu, dst, rank, size);
-    // a group's first record reserves the group; the others take their places behind it
-    uint32_t gb[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) gb[r] = ((uint32_t)r < n && rank[r] == 0u) ? atomicAdd(&lmsg[dst[r]], size[r]) : 0u;
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      uint32_t b = 0;
-#pragma unroll
-      for (int q = 0; q < R; ++q) b += (rank[q] == 0u && dst[q] == dst[r]) ? gb[q] : 0u;
-      place[r] = b + rank[r];
-    }
+    // each group takes its places in the block's range of its destination (LDS atomics)
+    n = sfl::env_groups(*P, e, rd, nu, dst, pos, size, place,
+                        [&](int d, uint32_t z) { return atomicAdd(&lmsg[d], z); });
   }
   // the launch totals of the envs that ran (a deferred env sat the local step out: its totals are the
   // last round's, already counted): one wave per block
@@ -217,12 +208,12 @@ __global__ void __launch_bounds__(64) k_part_compact(const sfl::SflPart* __restr
     sfl::PartMsg* x = P->msg_out + (size_t)dst[r] * (k + 1) + 1 + at;
     if (fits) {
       sfl::PartMsg y = (uint32_t)r < nu ? P->upd_st[(size_t)e * P->upd_env + r] : sfl::msg_of_req(P->req_st[e]);
-      y.kind |= rank[r] == 0u ? size[r] << 8 : 0u;
+      y.kind |= sfl::msg_tag(size[r], pos[r]);
       *x = y;
       if ((uint32_t)r == nu) P->req_ix[e] = (uint32_t)dst[r] * (k + 1) + 1u + at;  // (its reply lands there)
     } else if (at < k) {  // void records in the places below the segment's end
       x->genv = 0u;
-      x->kind = sfl::MSG_VOID | (1u << 8);
+      x->kind = sfl::MSG_VOID | sfl::msg_tag(1u, 0u);
     }
   }
   if ((bool)(flags & sfl::F_DEFER) != deferred) {
@@ -333,23 +324,61 @@ __device__ __forceinline__ void part_answer_fast(const sfl::SflMap& m, const sfl
   }
   out.action = arg;
 }
-// owner side of a round: every received group (one env's records for this rank, sfl_part.h part_owner_group) by
-// one thread, in order -- the env's updates, then the answer to its request.  A grid-stride loop up to each
-// segment's header count (the grid is bounded: a segment may be sized for the worst case, 17 records per env).
-// Round 4 ran this as three kernels (stage-0 updates in parallel, the later stages in one block, then the
-// answers) because records of one env were spread over the segment; with an env's records contiguous no
-// ordering is needed across threads.
-__global__ void __launch_bounds__(256) k_part_owner(const sfl::SflMap* __restrict__ m, const sfl::SflPart* __restrict__ P,
-                                                    const sfl::PartMsg* __restrict__ in, sfl::PartRep* __restrict__ out) {
-  const size_t k = P->k_msg, stride = (size_t)gridDim.x * blockDim.x;
-  for (int g = 0; g < P->world; ++g) {
-    const size_t base = (size_t)g * (k + 1);
+// owner side of a round (sfl_part.h part_owner_group's order per env): a block takes the groups that start in a
+// chunk of OWN_CHUNK records of a segment (its threads hold the chunk's records and the tails of groups that
+// run past its end), applies their update records stage by stage -- records of one stage touch distinct cells of
+// their env; a later stage (an arrival bonus, a later post of the same launch) may revisit a cell -- with a
+// block barrier between stages, then answers their requests.  One launch, every record on its own thread.
+// (Round 4 ran three kernels: stage-0 updates, the later stages in one block, the answers.  A first round-5 cut
+// walked each group on one thread: 30 us per round on the 8-rank rehearsal, the group's loads in one chain.)
+constexpr int OWN_CHUNK = 256;
+__global__ void __launch_bounds__(OWN_CHUNK) k_part_owner(const sfl::SflMap* __restrict__ m, const sfl::SflPart* __restrict__ P,
+                                                          const sfl::PartMsg* __restrict__ in, sfl::PartRep* __restrict__ out) {
+  constexpr int X = sfl::PART_GROUP_MAX - 1;  // a group reaches at most this far past its chunk
+  __shared__ uint32_t smax;
+  const size_t k = P->k_msg;
+  const uint32_t chunks = (uint32_t)((k + OWN_CHUNK - 1) / OWN_CHUNK), units = (uint32_t)P->world * chunks;
+  const uint32_t t = threadIdx.x;
+  for (uint32_t u = blockIdx.x; u < units; u += gridDim.x) {
+    const size_t base = (size_t)(u / chunks) * (k + 1);
     const size_t n = in[base].genv;
-    for (size_t i = 1 + (size_t)blockIdx.x * blockDim.x + threadIdx.x; i <= n; i += stride) {
-      const uint32_t len = sfl::msg_group(in[base + i].kind);
-      if (len == 0u || sfl::msg_type(in[base + i].kind) == sfl::MSG_VOID) continue;
-      sfl::part_owner_group(*m, *P, in + base + i, len, out + base + i,
-                            [&](const sfl::PartReq& r, sfl::PartRep& rep) { part_answer_fast(*m, *P, r, rep); });
+    const size_t lo = 1 + (size_t)(u % chunks) * OWN_CHUNK;
+    if (lo > n) continue;  // (block-uniform)
+    const size_t hi = min(lo + OWN_CHUNK, n + 1);
+    // this thread's records: lo + t, and for t < X the tail record hi + t; each one the block's if its group
+    // starts in [lo, hi)
+    sfl::PartMsg r[2];
+    bool mine[2];
+    uint32_t st[2];
+    const size_t ix[2] = {lo + t, hi + t};
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const bool in_range = q == 0 ? ix[0] < hi : (t < (uint32_t)X && ix[1] <= n);
+      r[q] = in[base + (in_range ? ix[q] : 0)];
+      const size_t gs = ix[q] - sfl::msg_pos(r[q].kind);
+      const uint32_t ty = sfl::msg_type(r[q].kind);
+      mine[q] = in_range && gs >= lo && gs < hi && ty != sfl::MSG_VOID;
+      st[q] = (mine[q] && (ty == sfl::MSG_UPD || ty == sfl::MSG_INSERT)) ? r[q].stage : 0u;
+    }
+    if (t == 0) smax = 0u;
+    __syncthreads();
+    const uint32_t top = max(st[0], st[1]);
+    if (top) atomicMax(&smax, top);
+    __syncthreads();
+    const uint32_t last = smax;
+    for (uint32_t s = 0; s <= last; ++s) {
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const uint32_t ty = sfl::msg_type(r[q].kind);
+        if (mine[q] && (ty == sfl::MSG_UPD || ty == sfl::MSG_INSERT) && st[q] == s) sfl::part_update_one(*m, *P, r[q]);
+      }
+      __syncthreads();  // (this stage's writes before the next stage's reads: one CU, one L1)
+    }
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const uint32_t ty = sfl::msg_type(r[q].kind);
+      if (mine[q] && (ty == sfl::MSG_REQ || ty == sfl::MSG_REQ_X))
+        part_answer_fast(*m, *P, sfl::req_of_msg(r[q]), out[base + ix[q]]);
     }
   }
 }
@@ -759,9 +788,9 @@ struct HipBackend {
     sfl::SflCtl c{};
     PartParams* pp = part_params(1, m, s, c, P);
     if (!pp) return;
-    const size_t n = (size_t)P.world * P.k_msg;
-    const unsigned blocks = (unsigned)std::min<size_t>((n + 255) / 256, 512);
-    k_part_owner<<<blocks, 256, 0, stream>>>(&pp->m, &pp->P, in, out);
+    const size_t units = (size_t)P.world * ((P.k_msg + OWN_CHUNK - 1) / OWN_CHUNK);
+    const unsigned blocks = (unsigned)std::min<size_t>(units, 1024);
+    k_part_owner<<<blocks, OWN_CHUNK, 0, stream>>>(&pp->m, &pp->P, in, out);
     check(hipGetLastError(), "k_part_owner");
   }
 };

@@ -12,7 +12,8 @@
 #if !defined(SFL_EXPERIMENT) &&                                                                                \
     (defined(SFL_X_NOTICK) || defined(SFL_X_NOPF) || defined(SFL_X_NORNG) || defined(SFL_AB_NO_QST) ||         \
      defined(SFL_AB_NO_TOUCH) || defined(SFL_AB_NO_SLOT) || defined(SFL_AB_LOAD2) || defined(SFL_AB_STORE2) ||   \
-     defined(SFL_X_NOSSQ) || defined(SFL_X_EPSCONST))
+     defined(SFL_X_NOSSQ) || defined(SFL_X_EPSCONST) || defined(SFL_AB_SLOT2) || defined(SFL_AB_QST2) ||         \
+     defined(SFL_AB_TOUCH2))
 #error "timing-only experiment switch without SFL_EXPERIMENT: build experiment libraries through build.py"
 #endif
 
@@ -67,6 +68,24 @@ constexpr bool kNoSeedSeqLoad = false;
 constexpr bool kEpsConst = true;  // epsilon = eps0 (no epsilon-table load)
 #else
 constexpr bool kEpsConst = false;
+#endif
+// Marginal cost of one write of the post step, with unchanged results: each write of the class issued a second
+// time, to the same address, behind a compiler barrier (so that it is not merged away).  The round-4 verdict's
+// slot write-back cache would remove one of a decision's two slot stores: SLOT2 bounds what that can gain.
+#ifdef SFL_AB_SLOT2
+constexpr bool kSlotTwice = true;  // every (switch, train) slot store of the fused post twice
+#else
+constexpr bool kSlotTwice = false;
+#endif
+#ifdef SFL_AB_QST2
+constexpr bool kQStoreTwice = true;  // the pending update's Q store twice
+#else
+constexpr bool kQStoreTwice = false;
+#endif
+#ifdef SFL_AB_TOUCH2
+constexpr bool kTouchTwice = true;  // the post's key-set inserts twice
+#else
+constexpr bool kTouchTwice = false;
 #endif
 }  // namespace xp
 }  // namespace sfl

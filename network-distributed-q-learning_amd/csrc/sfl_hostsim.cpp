@@ -116,28 +116,24 @@ struct HostBackend {
       const int rd = P.req_dst[e];
       const uint32_t nu = P.upd_n[e];
       int32_t dst[sfl::PART_GROUP_MAX];
-      uint32_t rank[sfl::PART_GROUP_MAX], size[sfl::PART_GROUP_MAX], at[sfl::PART_GROUP_MAX];
-      const uint32_t n = sfl::env_groups(P, e, rd, nu, dst, rank, size);
-      std::vector<uint32_t> gb(W, 0u);
-      for (uint32_t r = 0; r < n; ++r)
-        if (rank[r] == 0) {
-          gb[dst[r]] = nm[dst[r]];
-          nm[dst[r]] += size[r];
-        }
+      uint32_t pos[sfl::PART_GROUP_MAX], size[sfl::PART_GROUP_MAX], at[sfl::PART_GROUP_MAX];
+      const uint32_t n = sfl::env_groups(P, e, rd, nu, dst, pos, size, at, [&](int d, uint32_t z) {
+        const uint32_t b = nm[d];
+        nm[d] += z;
+        return b;
+      });
       bool fits = true;
-      for (uint32_t r = 0; r < n; ++r) {
-        at[r] = gb[dst[r]] + rank[r];
+      for (uint32_t r = 0; r < n; ++r)
         if (at[r] >= k) fits = false;
-      }
       for (uint32_t r = 0; r < n; ++r) {
         sfl::PartMsg& x = P.msg_out[(size_t)dst[r] * (k + 1) + 1 + at[r]];
         if (fits) {
           x = r < nu ? P.upd_st[(size_t)e * P.upd_env + r] : sfl::msg_of_req(P.req_st[e]);
-          if (rank[r] == 0) x.kind |= size[r] << 8;
+          x.kind |= sfl::msg_tag(size[r], pos[r]);
           if (r == nu) P.req_ix[e] = (uint32_t)dst[r] * (k + 1) + 1u + at[r];
         } else if (at[r] < k) {
           x.genv = 0u;
-          x.kind = sfl::MSG_VOID | (1u << 8);
+          x.kind = sfl::MSG_VOID | sfl::msg_tag(1u, 0u);
         }
       }
       if ((bool)(flags & sfl::F_DEFER) == fits) s.eflags[e] = flags ^ sfl::F_DEFER;
@@ -167,7 +163,7 @@ struct HostBackend {
 #pragma omp parallel for
       for (int64_t i = 1; i <= n; ++i) {
         const uint32_t len = sfl::msg_group(in[base + i].kind);
-        if (len == 0u || sfl::msg_type(in[base + i].kind) == sfl::MSG_VOID) continue;
+        if (sfl::msg_pos(in[base + i].kind) != 0u || sfl::msg_type(in[base + i].kind) == sfl::MSG_VOID) continue;
         sfl::part_owner_group(m, P, in + base + i, len, out + base + i,
                               [&](const sfl::PartReq& r, sfl::PartRep& rep) { sfl::part_answer_one(m, P, r, rep); });
       }

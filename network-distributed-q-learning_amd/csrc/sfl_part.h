@@ -73,12 +73,14 @@ struct PartUpd {
 };
 // a segment record (32 B): an update record (MSG_UPD / MSG_INSERT, the PartUpd fields) or a request
 // (MSG_REQ / MSG_REQ_X: genv, port, state as PartReq, amask in `j | stage << 8`).  kind bits 8-15: the
-// length of the env's group when this is its first record (0 inside a group); a deferred env's places
-// below the segment end carry MSG_VOID records of length 1.
+// length of the env's group, bits 16-23: the record's place in it (its group starts pos records before it);
+// a deferred env's places below the segment end carry MSG_VOID records (groups of one).
 enum : uint32_t { MSG_UPD = 0u, MSG_INSERT = 1u, MSG_VOID = 2u, MSG_REQ = 3u, MSG_REQ_X = 4u };
 typedef PartUpd PartMsg;
 SFL_FN constexpr uint32_t msg_type(uint32_t kind) { return kind & 0xFFu; }
 SFL_FN constexpr uint32_t msg_group(uint32_t kind) { return (kind >> 8) & 0xFFu; }
+SFL_FN constexpr uint32_t msg_pos(uint32_t kind) { return (kind >> 16) & 0xFFu; }
+SFL_FN constexpr uint32_t msg_tag(uint32_t len, uint32_t pos) { return (len << 8) | (pos << 16); }
 static_assert(sizeof(PartReq) == 16 && sizeof(PartRep) == 16 && sizeof(PartUpd) == 32, "record sizes");
 constexpr uint32_t PART_GROUP_MAX = PART_UPD_ENV_MAX + 1;  // records of one env in one segment, at most
 
@@ -230,7 +232,9 @@ SFL_FN void part_update_one(const SflMap& m, const SflPart& P, const PartUpd& u)
 // owner side: one env's group of a received segment, in order -- its update records as the env emitted
 // them (the pending update, key-set inserts, arrival bonuses: distr_q.py:325-362), then the answer to its
 // request, which may read a row those updates just wrote.  An env's records touch only that env's rows
-// (q_own / touched_own of its genv), so groups are independent of each other.
+// (q_own / touched_own of its genv), so groups are independent of each other.  (The host build walks a
+// group like this; k_part_owner applies a block's groups by update stage -- records of one stage touch
+// distinct cells of their env -- then answers, which is the same order per env.)
 template <class Answer>
 SFL_FN void part_owner_group(const SflMap& m, const SflPart& P, const PartMsg* g, uint32_t len, PartRep* rep,
                              Answer&& answer) {
@@ -243,25 +247,40 @@ SFL_FN void part_owner_group(const SflMap& m, const SflPart& P, const PartMsg* g
 
 // sender side: an env's staged records grouped per destination (k_part_compact, the host build's
 // part_compact).  Record r < nu is update r, to the owner of its row's switch; record nu the request, to rd
-// (if rd >= 0); dst = -1 past the last.  rank[r]: the record's place in its destination's group (emission
-// order, so the request comes last); size[r]: that group's length.  Returns the number of records.
+// (if rd >= 0); dst = -1 past the last.  For each destination the env writes to, reserve(d, size) returns the
+// place of its group in d's segment; place[r] = that + the record's place in the group (emission order, so
+// the request comes last), pos[r] its place in the group, size[r] the group's length.  Returns the number of
+// records.  (One pass per destination the env writes to -- usually one or two -- over bit masks.)
+template <class Reserve>
 SFL_FN uint32_t env_groups(const SflPart& P, uint32_t e, int rd, uint32_t nu, int32_t (&dst)[PART_GROUP_MAX],
-                           uint32_t (&rank)[PART_GROUP_MAX], uint32_t (&size)[PART_GROUP_MAX]) {
+                           uint32_t (&pos)[PART_GROUP_MAX], uint32_t (&size)[PART_GROUP_MAX],
+                           uint32_t (&place)[PART_GROUP_MAX], Reserve&& reserve) {
   const uint32_t n = nu + (rd >= 0 ? 1u : 0u);
 #pragma unroll
-  for (uint32_t r = 0; r < PART_GROUP_MAX; ++r)
-    dst[r] = r < nu ? P.owner[P.upd_st[(size_t)e * P.upd_env + r].port >> 2] : (r == nu && rd >= 0) ? rd : -1;
-#pragma unroll
   for (uint32_t r = 0; r < PART_GROUP_MAX; ++r) {
-    uint32_t k = 0, z = 0;
+    dst[r] = r < nu ? P.owner[P.upd_st[(size_t)e * P.upd_env + r].port >> 2] : (r == nu && rd >= 0) ? rd : -1;
+    pos[r] = size[r] = place[r] = 0u;
+  }
+  uint32_t left = (1u << n) - 1u;  // (n <= 17)
+  while (left) {
+    const uint32_t r0 = (uint32_t)__builtin_ctz(left);
+    int32_t d = -1;
+#pragma unroll
+    for (uint32_t q = 0; q < PART_GROUP_MAX; ++q) d = q == r0 ? dst[q] : d;
+    uint32_t mk = 0u;
+#pragma unroll
+    for (uint32_t q = 0; q < PART_GROUP_MAX; ++q) mk |= (q < n && dst[q] == d) ? (1u << q) : 0u;
+    const uint32_t z = (uint32_t)__builtin_popcount(mk);
+    const uint32_t b = reserve(d, z);
 #pragma unroll
     for (uint32_t q = 0; q < PART_GROUP_MAX; ++q) {
-      const bool same = q < n && dst[q] == dst[r];
-      k += (same && q < r) ? 1u : 0u;
-      z += same ? 1u : 0u;
+      if ((mk >> q) & 1u) {
+        pos[q] = (uint32_t)__builtin_popcount(mk & ((1u << q) - 1u));
+        size[q] = z;
+        place[q] = b + pos[q];
+      }
     }
-    rank[r] = k;
-    size[r] = z;
+    left &= ~mk;
   }
   return n;
 }

@@ -2097,15 +2097,19 @@ struct WEnv {
     // every global write of the step from one lane-0 region
     // (xp::kNo*: timing-only experiment builds that drop one class of store, sfl_experiment.h)
     if (lid() == 0) {
-      if (hp) {
-        if (!xp::kNoQStore) st(qbase(), (size_t)d.qoff_pend, nv);
-        if (!xp::kNoTouch) touch_row(d.row_pend);
-      }
-      if (!xp::kNoTouch && (d.touch_cur || (hp && d.sw != ps))) touch_row(d.row_cur);
-      if (!xp::kNoSlot) {
-        st(sbase(), slot_ix(d.sw, d.h), slot_make(PEND_NONE, slot_rew(d.slotword, epoch), epoch));
-        st(sbase(), slot_ix(d.next_sw, d.h),
-           slot_make(pend_make((uint32_t)d.sw, (uint32_t)d.slot, d.state, (uint32_t)d.j), d.r_new, epoch));
+      for (int rep = 0; rep < 2; ++rep) {  // (rep 1: the timing-only duplicate writes of sfl_experiment.h)
+        if (rep == 1 && !(xp::kQStoreTwice || xp::kTouchTwice || xp::kSlotTwice)) break;
+        if (rep == 1) asm volatile("" ::: "memory");
+        if (hp) {
+          if (!xp::kNoQStore && (rep == 0 || xp::kQStoreTwice)) st(qbase(), (size_t)d.qoff_pend, nv);
+          if (!xp::kNoTouch && (rep == 0 || xp::kTouchTwice)) touch_row(d.row_pend);
+        }
+        if (!xp::kNoTouch && (rep == 0 || xp::kTouchTwice) && (d.touch_cur || (hp && d.sw != ps))) touch_row(d.row_cur);
+        if (!xp::kNoSlot && (rep == 0 || xp::kSlotTwice)) {
+          st(sbase(), slot_ix(d.sw, d.h), slot_make(PEND_NONE, slot_rew(d.slotword, epoch), epoch));
+          st(sbase(), slot_ix(d.next_sw, d.h),
+             slot_make(pend_make((uint32_t)d.sw, (uint32_t)d.slot, d.state, (uint32_t)d.j), d.r_new, epoch));
+        }
       }
     }
     if (hp) pf_written(d.qoff_pend);

@@ -7,9 +7,15 @@ one device batch per seed (mapgen's stand-in for Flatland's sparse_rail_generato
 Writes the per-episode arrived trains / cumulative reward of every seed and a summary to compare with
 plot.ipynb cells 11 and 13 (mean arrived ~6 -> ~14.7 of 15 by ~6k episodes).
 
-Usage: python scripts/learning_curve.py OUT.json [--episodes N] [--seeds 64,65,...] [--host]
+Each seed's final Q-table (compact Q block + key-set bitmap) is recorded as a SHA-1, and --compare REF.json
+checks a run against another (e.g. the GPU against the host build): every episode's arrived trains, cumulative
+reward and decisions, and the final Q-table digests, equal.
+
+Usage: python scripts/learning_curve.py OUT.json [--episodes N] [--seeds 64,65,...] [--host] [--compare REF.json]
 """
 import argparse
+import gzip
+import hashlib
 import importlib
 import json
 import os
@@ -39,6 +45,8 @@ def main():
                          "stand-in with the same trains (mapgen.generate, 60 switches, 8 stations)")
     ap.add_argument("--rails", type=int, default=2, help="max_rails_between_cities (the sweep: 2)")
     ap.add_argument("--pairs", type=int, default=2, help="max_rail_pairs_in_city (the sweep: 2)")
+    ap.add_argument("--compare", default=None, help="a previous run's OUT.json(.gz): per-episode results and final "
+                                                    "Q-table digests must be equal")
     args = ap.parse_args()
     mapgen = importlib.import_module(PKG + ".mapgen")
     comp = importlib.import_module(PKG + ".compiler")
@@ -86,10 +94,14 @@ def main():
             done += n
             print(f"seed {seed}: {done} episodes, mean arrived (last {n}) {np.mean(out['arrived'][:, 0]):.2f} / "
                   f"{cm.T}, {time.time() - t0:.1f} s", flush=True)
+        q, t = b.q_raw(0)
+        qsha = hashlib.sha1(np.ascontiguousarray(q).tobytes() + np.ascontiguousarray(t).tobytes()).hexdigest()
+        kern = b.counters()
         b.close()
         res["seeds"][str(seed)] = dict(map=f"{sc.width}x{sc.height}, {cm.S} switches, {cm.T} trains, {cm.K} stations",
                                        arrived=arrived, cum_reward=cum, decisions=dec, arrived_exploit=arr_x,
-                                       cum_reward_exploit=cum_x, seconds=time.time() - t0)
+                                       cum_reward_exploit=cum_x, seconds=time.time() - t0, q_sha1=qsha,
+                                       library=os.path.basename(b.lib.path), kernel_variant=kern["kernel_variant"])
     A = np.array([v["arrived"] for v in res["seeds"].values()], dtype=float)
     w = max(1, args.episodes // 20)
     res["summary"] = {
@@ -100,6 +112,21 @@ def main():
         "trains": 15, "wall_s": time.time() - t_all,
         "decisions_total": int(sum(sum(v["decisions"]) for v in res["seeds"].values())),
     }
+    if args.compare:
+        op = gzip.open if args.compare.endswith(".gz") else open
+        ref = json.load(op(args.compare, "rt"))
+        cmp = {}
+        for k, v in res["seeds"].items():
+            r = ref["seeds"].get(k)
+            if r is None:
+                cmp[k] = "missing in the reference run"
+                continue
+            same = {f: v[f] == r[f] for f in ("arrived", "cum_reward", "decisions", "arrived_exploit", "cum_reward_exploit")}
+            same["q_sha1"] = v["q_sha1"] == r.get("q_sha1")
+            cmp[k] = "equal" if all(same.values()) else "DIFFERENT: " + ", ".join(f for f, ok in same.items() if not ok)
+        res["compare"] = {"reference": os.path.basename(args.compare), "seeds": cmp,
+                          "all_equal": all(x == "equal" for x in cmp.values())}
+        print(json.dumps(res["compare"]), flush=True)
     json.dump(res, open(args.out, "w"))
     print(json.dumps(res["summary"]), flush=True)
 

@@ -1,8 +1,13 @@
 """Summarise rocprofv3 PMC passes for the env kernel (k_run / k_wave) into a JSON (HBM traffic per launch, gfx950-corrected).
 
-FETCH_SIZE / WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE counts 64 B per 128-B request, i.e. half the
-bytes of a wide coalesced stream (MI355X_MICROARCH.md §HBM) — we apply that x2 correction and note
-that other access widths are uncalibrated.
+FETCH_SIZE / WRITE_SIZE are in KiB.  Calibrated for this kernel's access shapes (round 5,
+scripts/calib/fetch_calib.hip, profiles/r05_fetch_calib.json): on gfx950 every L2 read miss -- a scattered 4-, 8-,
+16-, 32-, 64- or 128-byte read as well as a coalesced 16-B/lane stream -- is ONE 128-byte memory request
+(TCC_EA0_RDREQ_128B = TCC_EA0_RDREQ, TCC_EA0_RDREQ_DRAM_32B = 4 x RDREQ), which FETCH_SIZE tallies as 64 B: the
+read bytes are exactly 2 x FETCH_SIZE.  Scattered 4- to 32-byte stores and 4-byte atomics are one 32-byte
+request each, which WRITE_SIZE counts exactly.  The bench kernel's own EA counters
+(profiles/r05_c3_ea_requests_per_decision.txt) show the same shape: all reads 128-B requests.
+When the TCC_EA0_* request counters are in the passes, the traffic is taken from them directly.
 Usage: python scripts/pmc_summary.py gpurun_out/<tag> profiles/<name>.json [bench.json of the same workload]
 The PMC passes run bench.py with its default workload; the bench line's config.workload is
 recorded so that bench.py reports the traffic only for that workload.
@@ -32,8 +37,12 @@ def main(src, dst, bench_json=None):
            "fetch_bytes_corrected": 2 * med.get("FETCH_SIZE", 0) * 1024,
            "write_bytes": med.get("WRITE_SIZE", 0) * 1024,
            "source_sha1": build.kernel_source_sha1(),
-           "note": "FETCH_SIZE x2 (gfx950 half-count of 128-B requests); uncalibrated for narrow scattered access"}
+           "note": "read bytes = FETCH_SIZE x 2: calibrated for this kernel's access shapes (every L2 read miss is a "
+                   "128-B request tallied as 64 B, profiles/r05_fetch_calib.json); WRITE_SIZE exact (32-B requests)"}
     out["traffic_bytes_per_launch"] = out["fetch_bytes_corrected"] + out["write_bytes"]
+    if "TCC_EA0_RDREQ_DRAM_32B" in med and "TCC_EA0_WRREQ_WRITE_DRAM_32B" in med:
+        out["traffic_from_ea_requests"] = 32.0 * (med["TCC_EA0_RDREQ_DRAM_32B"] + med["TCC_EA0_WRREQ_WRITE_DRAM_32B"]
+                                                  + med.get("TCC_EA0_WRREQ_ATOMIC_DRAM_32B", 0.0))
     if "TCC_HIT_sum" in med:
         out["l2_hit_rate"] = med["TCC_HIT_sum"] / max(1.0, med["TCC_HIT_sum"] + med["TCC_MISS_sum"])
     if "SQ_WAVE_CYCLES" in med:
@@ -46,6 +55,7 @@ def main(src, dst, bench_json=None):
         if "library" in bj:
             out["build_id"] = bj["library"]["build_id"]
             out["defines"] = bj["library"]["defines"]
+            out["source_sha1"] = out["build_id"] if not out["defines"] else out["source_sha1"]
         # VALU issue against the SIMDs' capacity: a wave64 VALU instruction takes 2 SIMD cycles (SIMD-32;
         # MI355X_MICROARCH.md cycle constants), 1,024 SIMDs at 2.4 GHz over the kernel's average duration
         ms = (bj.get("roofline") or {}).get("avg_kernel_ms")

@@ -1,0 +1,17 @@
+"""bench.py's reference-speed CPU baseline (cpu_oracle_baseline): the oracle's learn loop as one process per
+granted host core, one env each (the reference's one-process-per-seed scale-out, hyperparam_tuning.py:85-91),
+with the 1-core figure kept -- run here with two processes for a second each."""
+import bench
+
+
+def test_oracle_baseline_one_process_per_core():
+    pool = bench.start_oracle_pool(2)
+    try:
+        out = bench.cpu_oracle_baseline("c1", 1.0, pool=pool)
+    finally:
+        pool.close()
+        pool.join()
+    assert out["cores"] == 2 and out["kind"] == "port" and out["unit"] == "agent-env-steps/sec"
+    assert out["value"] > out["one_core_value"] > 0
+    assert "2 process(es)" in out["sample"] and "1 core:" in out["sample"]
+    assert bench.oracle_cores() >= 1
