@@ -42,7 +42,10 @@ enum : int {
   EB_PHASE = 0, EB_ELAPSED = 1, EB_EFLAGS = 2, EB_EPOCH = 3, EB_ERR = 4, EB_EP_T = 5, EB_N_TEST = 6, EB_N_MF = 7,
   EB_EP_DEC = 8, EB_EP_TICKS = 9, EB_STEP_CTR = 10 /* 2 */, EB_DEC_TOTAL = 12 /* 2 */, EB_CUM = 14 /* 2, f64 */,
   EB_RNG = 16 /* 5 x 2 */, EB_MASKS = 26 /* 4 x MAXW */, EB_DEC_DONE = 42 /* 2 */, EB_REQ_DST = 44, EB_UPD_N = 45,
-  EB_L_DEC = 46 /* 2 */, EB_L_TICKS = 48 /* 2 */, EB_L_BYTES = 50 /* 2 */, EB_USED = 52
+  EB_L_DEC = 46 /* 2 */, EB_L_TICKS = 48 /* 2 */, EB_L_BYTES = 50 /* 2 */,
+  // (round 5) the prefetch record of the decision whose request is open (F_REQ): the observe pass stages it and
+  // the next launch's apply pass reads it here instead of staging it again -- slot word (2), staged distances (3)
+  EB_PF = 52 /* 5 */, EB_USED = 57
 };
 constexpr int PART_EB = 64;
 

@@ -60,7 +60,7 @@ def test_gpus_4_host_rehearsal_runs_the_partitioned_leg():
     leg = res["partition_leg"]
     assert "error" not in leg, leg
     assert leg["world_size"] == 4 and leg["backend"] == "gloo" and leg["parity"] == "ok", leg
-    assert leg["parity_envs_checked"] == 8 and leg["collectives_per_round"] == 2 and "rehearsal" in leg
+    assert leg["parity_envs_checked"] >= 8 and leg["collectives_per_round"] == 2 and "rehearsal" in leg
     assert leg["rounds_per_step"] >= 25  # (the host build's local step sends every row: decisions + 1 rounds)
 
 
