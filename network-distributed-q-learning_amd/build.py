@@ -99,11 +99,11 @@ def build_hip(force: bool = False, verbose: bool = False, out: str = None, defin
         cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off",
                "-Wno-unused-result", "-Wno-unused-value", f'-DSFL_BUILD_ID="{build_id(defines, flags)}"',
                f'-DSFL_BUILD_DEFS="{defs}"', f'-DSFL_BUILD_FLAGS="{" ".join(flags)}"'] + \
-              [f"-D{d}" for d in defines] + list(flags) + ["-o", out + ".tmp", os.path.join(CSRC, "sfl.hip")]
+              [f"-D{d}" for d in defines] + list(flags) + ["-o", out + f".{os.getpid()}.tmp", os.path.join(CSRC, "sfl.hip")]
         if verbose:
             print(" ".join(cmd), flush=True)
         subprocess.run(cmd, check=True, cwd=CSRC)
-        os.replace(out + ".tmp", out)
+        os.replace(out + f".{os.getpid()}.tmp", out)
     return out
 
 
@@ -122,9 +122,9 @@ def build_hostsim(out_dir: str = None, force: bool = False, defines=(), flags=()
         cmd = ["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-fopenmp",
                f'-DSFL_BUILD_ID="{build_id(defines, flags)}"', f'-DSFL_BUILD_DEFS="{" ".join(sorted(defines))}"',
                f'-DSFL_BUILD_FLAGS="{" ".join(flags)}"'] + \
-              [f"-D{d}" for d in defines] + list(flags) + ["-o", out + ".tmp", os.path.join(CSRC, "sfl_hostsim.cpp")]
+              [f"-D{d}" for d in defines] + list(flags) + ["-o", out + f".{os.getpid()}.tmp", os.path.join(CSRC, "sfl_hostsim.cpp")]
         subprocess.run(cmd, check=True, cwd=CSRC)
-        os.replace(out + ".tmp", out)
+        os.replace(out + f".{os.getpid()}.tmp", out)
     return out
 
 

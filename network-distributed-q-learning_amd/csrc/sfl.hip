@@ -106,15 +106,23 @@ __global__ void __launch_bounds__(256) k_part_local(const sfl::SflMap* __restric
 // that place is deferred whole (F_DEFER; its places below the end get void records, its staged records go
 // again next round and the local step skips it until then).  arrays: the lane-per-env body (its scalars in
 // the SflState / SflPart arrays), else the wave kernels' per-env blocks (eblk).
-__global__ void __launch_bounds__(64) k_part_compact(const sfl::SflPart* __restrict__ P, const sfl::SflState* __restrict__ s,
+#ifndef SFL_COMPACT_BLOCK
+#define SFL_COMPACT_BLOCK 256  // threads (envs) per block of k_part_compact (64: -1.3 % on the 8-rank rehearsal)
+#endif
+__global__ void __launch_bounds__(SFL_COMPACT_BLOCK) k_part_compact(const sfl::SflPart* __restrict__ P, const sfl::SflState* __restrict__ s,
                                                      const sfl::SflCtl* __restrict__ c, int arrays) {
   constexpr int R = sfl::PART_GROUP_MAX;  // (register arrays: the loops over them are unrolled)
+  constexpr int EARLY = 2;                // update records read with the env's words (most envs stage <= 2)
+  constexpr int S_LDS = 1024;             // switches whose owners the block copies to LDS (more: read from the map)
   __shared__ uint32_t lmsg[256], bmsg[256];
-  __shared__ unsigned long long lsum[4];
+  __shared__ int32_t lown[S_LDS];
+  constexpr int NWV = SFL_COMPACT_BLOCK / 64;  // waves per block
+  __shared__ unsigned long long lsum[NWV][4];
   __shared__ uint32_t lopen, ldefer;
-  const int world = P->world;
+  const int world = P->world, S = P->n_sw;
   for (int i = threadIdx.x; i < world; i += blockDim.x) lmsg[i] = 0u;
-  __syncthreads();
+  if (threadIdx.x == 0) lopen = ldefer = 0u;
+  for (int i = threadIdx.x; i < S && i < S_LDS; i += blockDim.x) lown[i] = P->owner[i];
   const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
   const bool valid = e < s->E;
   int rd = -1;
@@ -124,16 +132,29 @@ __global__ void __launch_bounds__(64) k_part_compact(const sfl::SflPart* __restr
   // the wave kernel's per-env words (its scalar block, sfl_part.h EB_*), or the lane kernel's arrays
   const uint32_t* eb = (valid && !arrays) ? P->eblk + (size_t)e * sfl::PART_EB : nullptr;
   auto eb64 = [&](int i) { return (unsigned long long)eb[i] | ((unsigned long long)eb[i + 1] << 32); };
+  // the env's first update records and its request, read (clamped, unconditionally) with its words: their
+  // copies into the segment below need no second read, and their destinations no dependent load
+  const sfl::PartUpd* ust = P->upd_st + (size_t)(valid ? e : 0u) * P->upd_env;
+  sfl::PartUpd early[EARLY];
+#pragma unroll
+  for (int r = 0; r < EARLY; ++r) early[r] = ust[r < (int)P->upd_env ? r : 0];
+  const sfl::PartReq req = P->req_st[valid ? e : 0u];
   if (valid) {
     flags = eb ? eb[sfl::EB_EFLAGS] : s->eflags[e];
     rd = eb ? (int)eb[sfl::EB_REQ_DST] : P->req_dst[e];
     nu = eb ? eb[sfl::EB_UPD_N] : P->upd_n[e];
+  }
+  __syncthreads();  // (lown)
+  if (valid) {
+    auto own = [&](int sw) { return sw < S_LDS ? lown[sw] : P->owner[sw]; };
+#pragma unroll
+    for (int r = 0; r < R - 1; ++r)
+      if ((uint32_t)r < nu) dst[r] = own((r < EARLY ? early[r].port : ust[r].port) >> 2);
     // each group takes its places in the block's range of its destination (LDS atomics)
-    n = sfl::env_groups(*P, e, rd, nu, dst, pos, size, place,
-                        [&](int d, uint32_t z) { return atomicAdd(&lmsg[d], z); });
+    n = sfl::env_groups(rd, nu, dst, pos, size, place, [&](int d, uint32_t z) { return atomicAdd(&lmsg[d], z); });
   }
   // the launch totals of the envs that ran (a deferred env sat the local step out: its totals are the
-  // last round's, already counted): one wave per block
+  // last round's, already counted): wave sums, then one LDS slot per wave
   const bool ran = valid && !(flags & sfl::F_DEFER);
   unsigned long long a = !ran ? 0ull : eb ? eb64(sfl::EB_L_DEC) : c->launch_dec[e],
                      b = !ran ? 0ull : eb ? eb64(sfl::EB_L_TICKS) : c->launch_ticks[e],
@@ -145,16 +166,19 @@ __global__ void __launch_bounds__(64) k_part_compact(const sfl::SflPart* __restr
     d += __shfl_xor(d, off, 64);
     o |= __shfl_xor(o, off, 64);
   }
-  if (threadIdx.x == 0) {
-    lsum[0] = a;
-    lsum[1] = b;
-    lsum[2] = d;
-    lsum[3] = o;
+  if ((threadIdx.x & 63) == 0) {
+    const int w = threadIdx.x >> 6;
+    lsum[w][0] = a;
+    lsum[w][1] = b;
+    lsum[w][2] = d;
+    lsum[w][3] = o;
   }
   __syncthreads();
   for (int i = threadIdx.x; i < world; i += blockDim.x) bmsg[i] = lmsg[i] ? atomicAdd(P->cnt + i, lmsg[i]) : 0u;
   if (threadIdx.x < 4) {
-    const unsigned long long t = lsum[threadIdx.x];
+    unsigned long long t = 0;
+#pragma unroll
+    for (int w = 0; w < NWV; ++w) t = threadIdx.x == 3 ? (t | lsum[w][3]) : t + lsum[w][threadIdx.x];
     if (threadIdx.x == 3) {
       if (t) atomicOr((unsigned long long*)&P->sums[3], t);
     } else if (t) {
@@ -171,12 +195,18 @@ __global__ void __launch_bounds__(64) k_part_compact(const sfl::SflPart* __restr
   const bool deferred = valid && !fits;
   const bool open = valid && (rd >= 0 || deferred);
   const uint32_t n_open = __popcll(__ballot(open)), n_def = __popcll(__ballot(deferred));
+  if ((threadIdx.x & 63) == 0 && NWV > 1) {
+    if (n_open) atomicAdd(&lopen, n_open);
+    if (n_def) atomicAdd(&ldefer, n_def);
+  }
+  if (NWV > 1) __syncthreads();
   // the last block to get here writes the segment headers and hands the counts and totals to the
   // host copy (zeroing them for the next round): every block's reservations are done by then
   __shared__ bool last;
   if (threadIdx.x == 0) {
-    if (n_open) atomicAdd(P->cnt + world + 1, n_open);
-    if (n_def) atomicAdd(P->cnt + world + 2, n_def);
+    const uint32_t no = NWV > 1 ? lopen : n_open, nd = NWV > 1 ? ldefer : n_def;
+    if (no) atomicAdd(P->cnt + world + 1, no);
+    if (nd) atomicAdd(P->cnt + world + 2, nd);
   }
   __threadfence();  // (a workgroup-scope fence here measured +0.8 % on the C5 round; not worth the ordering risk)
   if (threadIdx.x == 0) last = atomicAdd(P->blocks_done, 1u) == gridDim.x - 1u;
@@ -207,7 +237,7 @@ __global__ void __launch_bounds__(64) k_part_compact(const sfl::SflPart* __restr
     const uint32_t at = bmsg[dst[r]] + place[r];
     sfl::PartMsg* x = P->msg_out + (size_t)dst[r] * (k + 1) + 1 + at;
     if (fits) {
-      sfl::PartMsg y = (uint32_t)r < nu ? P->upd_st[(size_t)e * P->upd_env + r] : sfl::msg_of_req(P->req_st[e]);
+      sfl::PartMsg y = (uint32_t)r < nu ? (r < EARLY ? early[r] : ust[r]) : sfl::msg_of_req(req);
       y.kind |= sfl::msg_tag(size[r], pos[r]);
       *x = y;
       if ((uint32_t)r == nu) P->req_ix[e] = (uint32_t)dst[r] * (k + 1) + 1u + at;  // (its reply lands there)
@@ -268,14 +298,33 @@ __global__ void __launch_bounds__(256) k_part_eblk(const sfl::SflState s, uint32
 // columns (8 bytes each), the block's width and offsets, then the row's columns, then the same comparisons in
 // the same order (row_max, max_action: bit-identical results).  Round 3: the generic version walks row_val
 // per action, a chain of dependent L2 reads per request (12.6 us of a 178-us round).
+// the map reads of an answer (they do not depend on the round's updates: k_part_owner issues them before its
+// stage loop, so the answer waits for the row only)
+struct AnsPre {
+  int na, w;
+  uint2 srcw, jw;
+  uint64_t qoff;
+  uint32_t rowb;
+};
+__device__ __forceinline__ AnsPre answer_pre(const sfl::SflMap& m, const sfl::SflPart& P, int port) {
+  const int sw = port >> 2;
+  AnsPre a;
+  a.na = m.sw_na[sw];
+  a.srcw = *(const uint2*)(m.act_src + (size_t)sw * 8);
+  a.jw = *(const uint2*)(m.act_j + (size_t)sw * 8);
+  a.w = m.q_w[port];
+  a.qoff = P.q_off_own[port];
+  a.rowb = P.row_own[port];
+  return a;
+}
 __device__ __forceinline__ void part_answer_fast(const sfl::SflMap& m, const sfl::SflPart& P, const sfl::PartReq& r,
-                                                 sfl::PartRep& out) {
-  const int port = r.port, sw = port >> 2, slot = port & 3;
-  const int na = m.sw_na[sw];
-  const uint2 srcw = *(const uint2*)(m.act_src + (size_t)sw * 8);
-  const uint2 jw = *(const uint2*)(m.act_j + (size_t)sw * 8);
-  const int w = m.q_w[port];
-  const double* row = P.q_own + (size_t)r.genv * P.q_own_per_env + P.q_off_own[port] + (size_t)r.state * (uint32_t)w;
+                                                 sfl::PartRep& out, const AnsPre& pre) {
+  const int port = r.port, slot = port & 3;
+  const int na = pre.na;
+  const uint2 srcw = pre.srcw;
+  const uint2 jw = pre.jw;
+  const int w = pre.w;
+  const double* row = P.q_own + (size_t)r.genv * P.q_own_per_env + pre.qoff + (size_t)r.state * (uint32_t)w;
   double rv[8];
 #pragma unroll
   for (int c = 0; c < 8; ++c) rv[c] = row[c < w ? c : 0];
@@ -306,7 +355,7 @@ __device__ __forceinline__ void part_answer_fast(const sfl::SflMap& m, const sfl
     out.action = -1;
     return;
   }
-  const uint32_t rid = P.row_own[port] + r.state;
+  const uint32_t rid = pre.rowb + r.state;
   atomicOr(&P.touched_own[(size_t)r.genv * P.own_words + (rid >> 5)], 1u << (rid & 31u));
   if ((r.amask >> best) & 1u) {
     out.action = best;
@@ -360,6 +409,12 @@ __global__ void __launch_bounds__(OWN_CHUNK) k_part_owner(const sfl::SflMap* __r
       mine[q] = in_range && gs >= lo && gs < hi && ty != sfl::MSG_VOID;
       st[q] = (mine[q] && (ty == sfl::MSG_UPD || ty == sfl::MSG_INSERT)) ? r[q].stage : 0u;
     }
+    AnsPre pre[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const uint32_t ty = sfl::msg_type(r[q].kind);
+      pre[q] = answer_pre(*m, *P, (mine[q] && (ty == sfl::MSG_REQ || ty == sfl::MSG_REQ_X)) ? (int)r[q].port : 0);
+    }
     if (t == 0) smax = 0u;
     __syncthreads();
     const uint32_t top = max(st[0], st[1]);
@@ -378,7 +433,7 @@ __global__ void __launch_bounds__(OWN_CHUNK) k_part_owner(const sfl::SflMap* __r
     for (int q = 0; q < 2; ++q) {
       const uint32_t ty = sfl::msg_type(r[q].kind);
       if (mine[q] && (ty == sfl::MSG_REQ || ty == sfl::MSG_REQ_X))
-        part_answer_fast(*m, *P, sfl::req_of_msg(r[q]), out[base + ix[q]]);
+        part_answer_fast(*m, *P, sfl::req_of_msg(r[q]), out[base + ix[q]], pre[q]);
     }
   }
 }
@@ -765,8 +820,9 @@ struct HipBackend {
     else if (m.T <= 64) k_part_local<2><<<blocks, 64, 0, stream>>>(&pp->m, &pp->s, &pp->c, &pp->P);
     else k_part_local<4><<<blocks, 64, 0, stream>>>(&pp->m, &pp->s, &pp->c, &pp->P);
     if (!check(hipGetLastError(), "k_part_local")) return -1;
-    // (64-thread blocks: a round's few records per env spread over every CU)
-    k_part_compact<<<(s.E + 63) / 64, 64, 0, stream>>>(&pp->P, &pp->s, &pp->c, variant > 0 ? 0 : 1);
+    // (256 envs per block: fewer blocks reserve places and count themselves done; 64 measured -1.3 %)
+    k_part_compact<<<(s.E + SFL_COMPACT_BLOCK - 1) / SFL_COMPACT_BLOCK, SFL_COMPACT_BLOCK, 0, stream>>>(&pp->P, &pp->s, &pp->c,
+                                                                                                  variant > 0 ? 0 : 1);
     check(hipEventRecord(ev1, stream), "event");
     // (no synchronisation here: the caller issues the launch totals and the count copies behind
     // it and syncs once; *ms is read with elapsed_ms() after that)

@@ -817,6 +817,7 @@ int part_config(Handle<B>* h, int rank, int world, const int32_t* owner, uint32_
   SflPart& P = h->part;
   P.rank = rank;
   P.world = world;
+  P.n_sw = S;
   P.env_base = env_base;
   P.E_tot = E_tot;
   // a segment holds one group per env of a source rank: its request and its update records to this

@@ -117,7 +117,8 @@ struct HostBackend {
       const uint32_t nu = P.upd_n[e];
       int32_t dst[sfl::PART_GROUP_MAX];
       uint32_t pos[sfl::PART_GROUP_MAX], size[sfl::PART_GROUP_MAX], at[sfl::PART_GROUP_MAX];
-      const uint32_t n = sfl::env_groups(P, e, rd, nu, dst, pos, size, at, [&](int d, uint32_t z) {
+      for (uint32_t r = 0; r < nu; ++r) dst[r] = P.owner[P.upd_st[(size_t)e * P.upd_env + r].port >> 2];
+      const uint32_t n = sfl::env_groups(rd, nu, dst, pos, size, at, [&](int d, uint32_t z) {
         const uint32_t b = nm[d];
         nm[d] += z;
         return b;

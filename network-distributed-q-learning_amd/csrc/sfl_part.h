@@ -42,10 +42,7 @@ enum : int {
   EB_PHASE = 0, EB_ELAPSED = 1, EB_EFLAGS = 2, EB_EPOCH = 3, EB_ERR = 4, EB_EP_T = 5, EB_N_TEST = 6, EB_N_MF = 7,
   EB_EP_DEC = 8, EB_EP_TICKS = 9, EB_STEP_CTR = 10 /* 2 */, EB_DEC_TOTAL = 12 /* 2 */, EB_CUM = 14 /* 2, f64 */,
   EB_RNG = 16 /* 5 x 2 */, EB_MASKS = 26 /* 4 x MAXW */, EB_DEC_DONE = 42 /* 2 */, EB_REQ_DST = 44, EB_UPD_N = 45,
-  EB_L_DEC = 46 /* 2 */, EB_L_TICKS = 48 /* 2 */, EB_L_BYTES = 50 /* 2 */,
-  // (round 5) the prefetch record of the decision whose request is open (F_REQ): the observe pass stages it and
-  // the next launch's apply pass reads it here instead of staging it again -- slot word (2), staged distances (3)
-  EB_PF = 52 /* 5 */, EB_USED = 57
+  EB_L_DEC = 46 /* 2 */, EB_L_TICKS = 48 /* 2 */, EB_L_BYTES = 50 /* 2 */, EB_USED = 52
 };
 constexpr int PART_EB = 64;
 
@@ -89,6 +86,7 @@ constexpr uint32_t PART_GROUP_MAX = PART_UPD_ENV_MAX + 1;  // records of one env
 
 struct SflPart {
   int32_t rank, world;
+  int32_t n_sw;               // switches of the map (owner[] entries)
   const uint32_t* local_sw;   // [S] 1: the wave kernel reads / writes this switch's rows here directly
                               // (its owner is this rank; all 0: every row operation as a message)
   uint32_t env_base;  // global index of local env 0
@@ -249,19 +247,19 @@ SFL_FN void part_owner_group(const SflMap& m, const SflPart& P, const PartMsg* g
 }
 
 // sender side: an env's staged records grouped per destination (k_part_compact, the host build's
-// part_compact).  Record r < nu is update r, to the owner of its row's switch; record nu the request, to rd
-// (if rd >= 0); dst = -1 past the last.  For each destination the env writes to, reserve(d, size) returns the
-// place of its group in d's segment; place[r] = that + the record's place in the group (emission order, so
-// the request comes last), pos[r] its place in the group, size[r] the group's length.  Returns the number of
-// records.  (One pass per destination the env writes to -- usually one or two -- over bit masks.)
+// part_compact).  Record r < nu is update r, to the owner of its row's switch (dst[r], filled by the caller);
+// record nu the request, to rd (if rd >= 0); dst = -1 past the last.  For each destination the env writes to,
+// reserve(d, size) returns the place of its group in d's segment; place[r] = that + the record's place in the
+// group (emission order, so the request comes last), pos[r] its place in the group, size[r] the group's length.
+// Returns the number of records.  (One pass per destination the env writes to -- usually one or two -- over
+// bit masks.)
 template <class Reserve>
-SFL_FN uint32_t env_groups(const SflPart& P, uint32_t e, int rd, uint32_t nu, int32_t (&dst)[PART_GROUP_MAX],
-                           uint32_t (&pos)[PART_GROUP_MAX], uint32_t (&size)[PART_GROUP_MAX],
-                           uint32_t (&place)[PART_GROUP_MAX], Reserve&& reserve) {
+SFL_FN uint32_t env_groups(int rd, uint32_t nu, int32_t (&dst)[PART_GROUP_MAX], uint32_t (&pos)[PART_GROUP_MAX],
+                           uint32_t (&size)[PART_GROUP_MAX], uint32_t (&place)[PART_GROUP_MAX], Reserve&& reserve) {
   const uint32_t n = nu + (rd >= 0 ? 1u : 0u);
 #pragma unroll
   for (uint32_t r = 0; r < PART_GROUP_MAX; ++r) {
-    dst[r] = r < nu ? P.owner[P.upd_st[(size_t)e * P.upd_env + r].port >> 2] : (r == nu && rd >= 0) ? rd : -1;
+    dst[r] = r < nu ? dst[r] : (r == nu && rd >= 0) ? rd : -1;
     pos[r] = size[r] = place[r] = 0u;
   }
   uint32_t left = (1u << n) - 1u;  // (n <= 17)

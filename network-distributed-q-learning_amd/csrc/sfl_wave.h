@@ -890,13 +890,6 @@ struct WEnv {
         const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute((EB_RNG + 2 * l + 1) << 2, (int)eb_w);
         if (lane < 5) lrng[lane] = (uint64_t)lo | ((uint64_t)hi << 32);
       }
-      if (flags & F_REQ) {  // the open request's prefetch record, staged by the observe pass (store_eblk)
-        lpf[1] = __longlong_as_double((long long)ebw64(EB_PF));
-        lpi[0] = ebw(EB_PF + 2);
-        lpi[1] = ebw(EB_PF + 3);
-        lpi[2] = ebw(EB_PF + 4);
-        pf_ok = true;
-      }
       cum = (int64_t)__longlong_as_double((long long)ebw64(EB_CUM));
       n_mf = (int32_t)ebw(EB_N_MF);
       ep_dec = (int32_t)ebw(EB_EP_DEC);
@@ -1063,11 +1056,8 @@ struct WEnv {
       mwords(2, fl_mask);
       mwords(3, mf_mask);
       static_assert(EB_PHASE == 0 && EB_EP_DEC == 8 && EB_STEP_CTR == 10 && EB_RNG == 16 && EB_MASKS == 26 &&
-                        EB_DEC_DONE == 42 && EB_PF == 52 && EB_USED == 57 && MAXW == 4,
+                        EB_DEC_DONE == 42 && EB_USED == 52 && MAXW == 4,
                     "block layout");
-      // (read before the block's puts: the record of record index 0, PART's only one)
-      const uint64_t pf_slot = (uint64_t)__double_as_longlong(lpf[1]);
-      const uint32_t pf_w0 = lpi[0], pf_w1 = lpi[1], pf_w2 = lpi[2];
       put4(0, (uint32_t)phase, (uint32_t)now, flags, epoch);
       put4(4, err, (uint32_t)ep_t, (uint32_t)n_test, (uint32_t)n_mf);
       put4(8, (uint32_t)ep_dec, (uint32_t)ep_ticks, (uint32_t)step_ctr, 0u);
@@ -1081,8 +1071,6 @@ struct WEnv {
       put4(40, lo(mw[3][1]), hi(mw[3][1]), lo((uint64_t)dec_done), hi((uint64_t)dec_done));
       put4(44, (uint32_t)req_dst, upd_n, lo(l_dec), hi(l_dec));
       put4(48, lo(l_ticks), hi(l_ticks), lo(l_bytes), hi(l_bytes));
-      put4(52, lo(pf_slot), hi(pf_slot), pf_w0, pf_w1);
-      put4(56, pf_w2, 0u, 0u, 0u);
       const uint32_t v = sg[lane < EB_USED ? lane : 0];
       if (lane < EB_USED) st(P->eblk, (size_t)e * PART_EB + (uint32_t)lane, v);
     }
@@ -1710,16 +1698,13 @@ struct WEnv {
     // agent_iter: lowest queued train (switch_env.py:418-421, 616-622)
     // (PART observe pass: the observation needs one distance, looked up directly below; the
     // staging waits for the apply pass in the next launch)
-    // (PART: the observe pass stages this train's record too -- the observation reads its distance there -- and
-    // the record travels in the env's scalar block to the apply pass of the next launch, which then stages
-    // nothing: load() restores it and sets pf_ok.  Round 4's apply pass staged it again, one to three dependent
-    // loads at the head of every launch: 49 % of k_wave2_part's wave time by the phase laps.)
-    if (!pf_ok || (RING && pf_n >= PF_SLOTS)) {
+    // (PART observe pass: no staging.  Round 5 measured carrying the observe pass's record to the apply pass in the
+    // env's scalar block instead of restaging it: 95.2 M vs 95.8 M per GPU on the 8-rank rehearsal -- the apply
+    // pass's staging overlaps its state load; not kept.)
+    if ((!pf_ok || (RING && pf_n >= PF_SLOTS)) && !observe_only) {
       prefetch(greedy);
       pf_ok = !PART;  // (PART stages only this decision's train: the next one stages its own)
       SFL_PCNT(3);
-    } else if constexpr (PART) {
-      pf_ok = false;  // the restored record is this decision's; the next decision of the launch stages its own
     }
     SFL_LAP(0);
     SFL_PCNT(8);
@@ -1774,7 +1759,7 @@ struct WEnv {
     const uint32_t b = trl(bits, h);
     const int32_t p0 = trl(pos, h);
     const int32_t ed = tr[0], la = tr[1], k = tr[2];
-    const int32_t d_obs = dist_staged(d16_lo(U(pfd01[0])));
+    const int32_t d_obs = observe_only ? dist(k, p0, (int)tb_dir(b)) : dist_staged(d16_lo(U(pfd01[0])));
     const int32_t dl = now - la + d_obs;
     const int32_t avail = la - ed;
     const uint32_t lvl = dl <= 0 ? 0u : (dl <= avail * m.delay_thr ? 1u : 2u);
