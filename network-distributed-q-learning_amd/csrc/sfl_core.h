@@ -126,6 +126,15 @@ SFL_FN uint32_t mod_small(uint64_t x, uint32_t n, uint64_t M) {
   return (uint32_t)r;
 }
 
+// mf_propose's integer forms of the map's malfunction parameters (set when the map is built, sfl_engine.h)
+inline void mf_prepare(SflMap& m) {
+  const double R = ldexp(m.mf_rate, 53);
+  m.mf_thresh = !(m.mf_rate > 0.0) ? 0ull : (R >= 9007199254740992.0 ? (1ull << 53) : (uint64_t)ceil(R));
+  const int64_t n = (int64_t)m.mf_max - (int64_t)m.mf_min + 1;
+  m.mf_n = (n >= 1 && n < (1ll << 32)) ? (uint32_t)n : 0u;
+  m.mf_magic = m.mf_n ? ~0ull / m.mf_n : 0ull;
+}
+
 // the malfunction proposed to train h of env e at step t, given its state and counter (both streams)
 SFL_FN uint32_t mf_propose(const SflMap& m, uint64_t seed, uint32_t e, int32_t t, int h) {
   if (m.mf_steps > 0) {

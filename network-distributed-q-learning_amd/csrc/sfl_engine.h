@@ -214,13 +214,7 @@ int create(const sfl_map_desc* md, const sfl_hparams* hp, uint32_t n_envs, const
   m.mf_rate = md->mf_rate;
   m.mf_min = md->mf_min;
   m.mf_max = md->mf_max;
-  {  // mf_propose's integer forms of u < mf_rate and of the duration's modulo (sfl_core.h)
-    const double R = ldexp(md->mf_rate, 53);
-    m.mf_thresh = !(md->mf_rate > 0.0) ? 0ull : (R >= 9007199254740992.0 ? (1ull << 53) : (uint64_t)ceil(R));
-    const int64_t n = (int64_t)md->mf_max - (int64_t)md->mf_min + 1;
-    m.mf_n = (n >= 1 && n < (1ll << 32)) ? (uint32_t)n : 0u;
-    m.mf_magic = m.mf_n ? ~0ull / m.mf_n : 0ull;
-  }
+  mf_prepare(m);  // (mf_propose's integer forms of u < mf_rate and of the duration's modulo)
   m.delay_thr = md->delay_threshold;
   m.gamma = hp->gamma;
   m.eps0 = hp->epsilon;

@@ -197,6 +197,19 @@ int sflh_set_threads(int n) {
   if (n > 0) omp_set_num_threads(n);
   return omp_get_max_threads();
 }
+// the counter-based malfunction proposal (mf_propose with the map's integer threshold / modulo forms) for n
+// (tick, handle) pairs: tests/test_rng.py checks it against the oracle's float compare and 64-bit remainder
+int sflh_mf_propose(double rate, int32_t mf_min, int32_t mf_max, uint64_t seed, uint32_t n, const int32_t* ticks,
+                    const int32_t* handles, uint32_t* out) {
+  sfl::SflMap m{};
+  m.mf_rate = rate;
+  m.mf_min = mf_min;
+  m.mf_max = mf_max;
+  m.mf_steps = 0;
+  sfl::mf_prepare(m);
+  for (uint32_t i = 0; i < n; ++i) out[i] = sfl::mf_propose(m, seed, 0u, ticks[i], handles[i]);
+  return 0;
+}
 int sflh_mf_draw(uint64_t seed, uint64_t tick, uint64_t handle, uint64_t* z) {
   *z = sfl::mf_draw(seed, tick, handle);
   return 0;
