@@ -109,12 +109,10 @@ struct SflMap {
   int32_t mf_steps;
 };
 
-#ifndef SFL_MF_FASTMOD
-#define SFL_MF_FASTMOD 1  // (tuning A/B: 0 = the f64 compare and the 64-bit `%`)
-#endif
 // x % n for 1 <= n < 2^32 with M = floor((2^64 - 1) / n): q = hi64(x * M) is floor(x / n) or one less (M is
 // within 1 of 2^64 / n and x < 2^64), so one correction makes the remainder exact.  On the GPU the 64-bit `%`
-// is a ~200-instruction expansion; this is a 64 x 64 high product and a few integer ops.
+// is a ~200-instruction expansion; this is a 64 x 64 high product and a few integer ops (c3: +0.7 %, same box,
+// profiles/r05i_mf_fastmod_ab.txt).
 SFL_FN uint32_t mod_small(uint64_t x, uint32_t n, uint64_t M) {
 #if defined(__HIP_DEVICE_COMPILE__)
   const uint64_t q = __umul64hi(x, M);
@@ -144,17 +142,11 @@ SFL_FN uint32_t mf_propose(const SflMap& m, uint64_t seed, uint32_t e, int32_t t
   if (!(m.mf_rate > 0.0)) return 0u;
   const uint64_t z = mf_draw(seed, (uint64_t)t, (uint64_t)h);
   // u = (z >> 11) * 2^-53 is exact, so u < mf_rate  <=>  (z >> 11) < ceil(mf_rate * 2^53)  (oracle/flatland_lite.py)
-#if SFL_MF_FASTMOD
   if ((z >> 11) >= m.mf_thresh) return 0u;
   const uint64_t x = mix64(z ^ 0xA0761D6478BD642Full);
   const uint32_t r = m.mf_n ? mod_small(x, m.mf_n, m.mf_magic)
                             : (uint32_t)(x % (uint64_t)(m.mf_max - m.mf_min + 1));  // (mf_max < mf_min: as before)
   return (uint32_t)(m.mf_min + (int32_t)r) + 1u;
-#else
-  const double u = (double)(z >> 11) * (1.0 / 9007199254740992.0);
-  if (!(u < m.mf_rate)) return 0u;
-  return (uint32_t)(m.mf_min + (int32_t)(mix64(z ^ 0xA0761D6478BD642Full) % (uint64_t)(m.mf_max - m.mf_min + 1))) + 1u;
-#endif
 }
 
 struct SflState {
