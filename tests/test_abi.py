@@ -182,3 +182,14 @@ def test_flags_only_build_is_an_experiment_named_by_its_flags(tmp_path):
 def test_product_library_carries_no_flags():
     assert build.built_flags(build.build_hip()) == ""
     assert build.built_flags(build.build_hostsim()) == ""
+
+
+def test_integration_stub_names_the_current_abi():
+    """INTEGRATION.md's ctypes stub (the binding a switchfl maintainer adds) asserts the header's ABI version."""
+    import re
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    hdr = open(os.path.join(root, "include", "sfl.h")).read()
+    want = int(re.search(r"#define SFL_ABI_VERSION (\d+)", hdr).group(1))
+    doc = open(os.path.join(root, "INTEGRATION.md")).read()
+    got = [int(x) for x in re.findall(r"sfl_abi_version\(\) == (\d+)", doc)]
+    assert got and all(v == want for v in got), (got, want)
