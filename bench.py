@@ -345,6 +345,10 @@ def main():
                     help="with --partition on one rank: only the switches of block 0 of a V-rank partition are "
                          "decided on in place, the rest travel as messages (a V-rank job's per-GPU traffic, without "
                          "the transfers)")
+    ap.add_argument("--cohorts", type=int, default=None,
+                    help="--partition: the rank's envs as this many independent partitioned jobs whose rounds are "
+                         "issued alternately (partition.CohortPipeline), so one cohort's exchange and owner step "
+                         "overlap another's local step (default: %d on the GPU, 1 on the host build)" % 3)
     ap.add_argument("--partition", action="store_true",
                     help="graph-partitioned mode (BASELINE configs[4]): switch agents owned by ranks, RCCL all-to-all "
                          "of row lookups and updates; defaults to --config c5 --envs 16384 (238 GB of owned Q rows per GPU)")
@@ -517,6 +521,12 @@ def bench_partition(args):
         dist.destroy_process_group()
 
 
+# --partition's default cohorts on the GPU (round 5, profiles/r05m_part_cohorts.txt: 1 / 2 / 3 / 4 cohorts
+# 98.6 / 101.1 / 103.1 / 73.4 M per GPU on the 8-rank rehearsal; 4 cohort streams and torch's own exceed the
+# process's 4 hardware queues)
+PARTITION_COHORTS = 3
+
+
 def partition_run(args, par, dist, world, rank, dev, red_dev, devices, host: bool = False):
     """The partitioned bench on the ranks of `dist` (collective); the bench line's dict on rank 0, else None.
     host: the --rehearse-on-host run (the host build of the kernel body, CPU buffers, gloo)."""
@@ -536,8 +546,12 @@ def partition_run(args, par, dist, world, rank, dev, red_dev, devices, host: boo
         _lib = importlib.import_module(PKG + "._lib")
         lib = _lib.Lib(importlib.import_module(PKG + ".build").build_hostsim())
         lib.check_fresh()
-    pb = part.PartitionedBatch(cm, HP, seeds, rank * E, world * E, rank=rank, world=world, dist=dist, device=dev,
-                               lib=lib, buffer_device="cpu" if host else "cuda", local_rows=local)
+    cohorts = getattr(args, "cohorts", None)
+    cohorts = min(E, cohorts if cohorts else (1 if host else PARTITION_COHORTS))
+    kw = dict(rank=rank, world=world, dist=dist, device=dev, lib=lib, buffer_device="cpu" if host else "cuda",
+              local_rows=local)
+    pb = (part.CohortPipeline(cm, HP, seeds, rank * E, world * E, cohorts=cohorts, **kw) if cohorts > 1
+          else part.PartitionedBatch(cm, HP, seeds, rank * E, world * E, **kw))
     pb.learn_begin()
     pb.apply_qinit()
     for _ in range(args.warmup):
@@ -606,6 +620,7 @@ def partition_run(args, par, dist, world, rank, dev, red_dev, devices, host: boo
                        "count_reads_per_step": (r1 - r0) / max(1, args.steps),
                        "segment_records": pb.k_msg, "segment_capacity": pb.cap_msg,
                        "collectives_per_round": 2 if world > 1 else 0,
+                       "cohorts": cohorts,
                        "deferrals": pb.deferrals - d0,
                        "parallelism": f"env-batch dp{world} x switch-agent partition {world}"},
             "library": library_info(pb.lib),
@@ -629,8 +644,10 @@ def partition_run(args, par, dist, world, rank, dev, red_dev, devices, host: boo
 # (rank 0) or after the watchdog (the other ranks wait for it, so that the launcher does not stop rank 0 before it
 # has printed), on a hang by the watchdog (rank 0 first).  SFL_NO_PARTITION_LEG=1 skips it.  --rehearse-on-host
 # runs it on the host build (PARTITION_LEG_HOST).
+# (one cohort: the leg is the first contact of the exchange with RCCL, so it runs the single-job path with one
+# communicator; --partition --cohorts N measures the cohort pipeline)
 PARTITION_LEG = dict(config="c5", envs=2048, decisions=256, steps=4, warmup=2, verify_envs=8, remote_rows=False,
-                     virtual_ranks=0)
+                     virtual_ranks=0, cohorts=1)
 PARTITION_LEG_HOST = dict(PARTITION_LEG, envs=4, decisions=24, steps=1)
 PARTITION_LEG_TIMEOUT_S = 300.0
 PARTITION_LEG_FAILED = 3
@@ -675,7 +692,7 @@ def partition_leg(par, dist, world, rank, dev, red_dev, devices, res, emit, host
            "value": leg["value"], "unit": leg["unit"], "backend": leg["backend"], "world_size": leg["world_size"],
            "rounds_per_step": cfgd["rounds_per_step"], "checkpoints_per_step": cfgd["checkpoints_per_step"],
            "count_reads_per_step": cfgd["count_reads_per_step"], "segment_records": cfgd["segment_records"],
-           "collectives_per_round": cfgd.get("collectives_per_round"),
+           "collectives_per_round": cfgd.get("collectives_per_round"), "cohorts": cfgd.get("cohorts"),
            "deferrals": cfgd["deferrals"], "parity": leg.get("parity"),
            "parity_envs_checked": leg.get("parity_envs_checked"), "wall_s": time.perf_counter() - t0}
     if host:

@@ -83,7 +83,7 @@ def check_batch(b: Batch, hp: dict, pick: Sequence[int], schedule: Sequence[int]
 
 def check_partition(pb, hp: dict, pick_global: Sequence[int], seed_of, schedule: Sequence[int],
                     host_lib: _lib.Lib, **kw) -> List[str]:
-    """Mismatches of a partitioned batch ``pb`` (partition.PartitionedBatch) for the job's global envs
+    """Mismatches of a partitioned batch ``pb`` (partition.PartitionedBatch or CohortPipeline) for the job's global envs
     ``pick_global``: this rank's owned rows (and their key-set bits) vs a fused host run of those envs'
     seeds; the env state too for the sampled envs this rank simulates."""
     cm = pb.cm
@@ -109,9 +109,9 @@ def check_partition(pb, hp: dict, pick_global: Sequence[int], seed_of, schedule:
             rbits = np.unpackbits(tr.view(np.uint8), bitorder="little")[:cm.rows_per_env].astype(bool)
             if not np.array_equal(bits, rbits & own_rows):
                 bad.append(f"env {ge}: owned key-set bits")
-            le = ge - pb.env_base
-            if 0 <= le < pb.E:
-                bad += [f"env {ge}: {d}" for d in _state_diff(env_state(pb.batch, le), env_state(ref, i))]
+            sim = pb.sim_env(ge)  # (batch, local env) if this rank simulates it
+            if sim is not None:
+                bad += [f"env {ge}: {d}" for d in _state_diff(env_state(sim[0], sim[1]), env_state(ref, i))]
     finally:
         ref.close()
     return bad

@@ -26,6 +26,7 @@ also agree on the next segment sizes -- no host synchronisation in the rounds be
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes as C
 from collections import deque
 from typing import List, Optional, Sequence
@@ -83,7 +84,8 @@ class PartitionedBatch:
                  rank: int = 0, world: int = 1, dist=None, lib: Optional[_lib.Lib] = None, device: int = 0,
                  owner: Optional[np.ndarray] = None, upd_per_env: int = 16, ntab: Optional[int] = None,
                  buffer_device: str = "cuda", local_rows=True, malfunction_stream: str = "counter",
-                 delay_threshold: int = 20, k_init: Optional[int] = None, checkpoint_every_round: bool = False):
+                 delay_threshold: int = 20, k_init: Optional[int] = None, checkpoint_every_round: bool = False,
+                 group=None):
         import torch
         self.torch = torch
         kw = {} if ntab is None else dict(ntab=ntab)
@@ -92,6 +94,7 @@ class PartitionedBatch:
         self.batch = Batch(cm, hp, seeds, lib=lib, device=device, **kw)
         self.lib = self.batch.lib
         self.cm, self.rank, self.world, self.dist = cm, int(rank), int(world), dist
+        self.group = group  # the process group of this job's collectives (None: the default group)
         self.E = self.batch.E
         self.env_base, self.envs_total = int(env_base), int(envs_total)
         self.owner = np.ascontiguousarray(owner if owner is not None else partition_switches(cm, world), np.int32)
@@ -167,21 +170,21 @@ class PartitionedBatch:
         if self.dist is None or self.world == 1:
             return self.E, self.E
         torch = self.torch
-        dev = "cuda" if (buffer_device == "cuda" and self.dist.get_backend() != "gloo") else "cpu"
+        dev = "cuda" if (buffer_device == "cuda" and self.dist.get_backend(self.group) != "gloo") else "cpu"
         t = torch.tensor([self.E, -self.E], dtype=torch.int64, device=dev)
         mx = t.clone()
-        self.dist.all_reduce(mx, op=self.dist.ReduceOp.MAX)
+        self.dist.all_reduce(mx, op=self.dist.ReduceOp.MAX, group=self.group)
         sm = torch.tensor([self.E], dtype=torch.int64, device=dev)
-        self.dist.all_reduce(sm)
+        self.dist.all_reduce(sm, group=self.group)
         return int(mx[0]), int(sm[0])
 
     def _all_max(self, vals):
         """Element-wise MAX of per-rank integer vectors over the job (every rank gets the same answer)."""
         if self.dist is None or self.world == 1:
             return list(vals)
-        dev = "cuda" if (self.on_gpu and self.dist.get_backend() != "gloo") else "cpu"
+        dev = "cuda" if (self.on_gpu and self.dist.get_backend(self.group) != "gloo") else "cpu"
         t = self.torch.tensor(list(vals), dtype=self.torch.int64, device=dev)
-        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX, group=self.group)
         return t.cpu().tolist()
 
     # ---- the reference's learn() set-up, on the partitioned tables ----------------------------
@@ -221,12 +224,12 @@ class PartitionedBatch:
             if r.data_ptr() != s_.data_ptr():
                 r.copy_(s_)
             return
-        if self.on_gpu and self.dist.get_backend() == "gloo":
+        if self.on_gpu and self.dist.get_backend(self.group) == "gloo":
             rc = self.torch.empty(r.numel(), dtype=self.torch.uint8)
-            self.dist.all_to_all_single(rc, s_.cpu())
+            self.dist.all_to_all_single(rc, s_.cpu(), group=self.group)
             r.copy_(rc)
         else:
-            self.dist.all_to_all_single(r, s_)
+            self.dist.all_to_all_single(r, s_, group=self.group)
 
     def _read_counts(self):
         """This rank's counts since the previous checkpoint (sfl_part_counts: the checkpoint's host
@@ -245,10 +248,14 @@ class PartitionedBatch:
     def step(self, decisions_per_env: int) -> int:
         """Advance every local env by ``decisions_per_env`` learning decisions (the sfl_step contract);
         returns the number of rounds.  Collective over the ranks."""
-        if self.stream is None:
-            return self._step(decisions_per_env)
-        with self.torch.cuda.stream(self.stream):
-            return self._step(decisions_per_env)
+        with self.stream_context():
+            for _ in self.rounds_of_step(decisions_per_env):
+                pass
+        return self.last_rounds
+
+    def stream_context(self):
+        """The context the job's work is issued in: its own stream on the GPU."""
+        return contextlib.nullcontext() if self.stream is None else self.torch.cuda.stream(self.stream)
 
     def _checkpoint(self, r: int, last: int) -> bool:
         """Rounds after which the host reads the counts: 1, 2, 4, ..., 32, every 32nd, the round a step
@@ -257,7 +264,12 @@ class PartitionedBatch:
         return (self.checkpoint_every_round or (r & (r - 1) == 0 and r <= 32) or r % 32 == 0 or r == last
                 or (r > last and (r - last) % 8 == 0))
 
-    def _step(self, decisions_per_env: int) -> int:
+    def rounds_of_step(self, decisions_per_env: int):
+        """One step as a generator (issue it in ``stream_context()``): each iteration issues one round
+        (local step, message all-to-all, owner step, reply all-to-all) without waiting for it and yields;
+        a checkpoint round's counts are read at the next iteration, so that a caller alternating several
+        jobs (CohortPipeline) issues the others' rounds before this one's host wait.  ``last_rounds``
+        holds the step's rounds when the generator ends."""
         d = self.lib.dll
         h = self.batch.h
         W = self.world
@@ -286,6 +298,7 @@ class PartitionedBatch:
             if failed and W > 1:
                 self._view(self.rep_send, self.k_msg, rp).zero_()
             self._a2a(self.rep_recv, self.rep_send, self.k_msg, rp)
+            yield rounds
             if not self._checkpoint(rounds, last) and rounds < limit:
                 continue
             self.checkpoints += 1
@@ -307,7 +320,12 @@ class PartitionedBatch:
             if W > 1:
                 self.set_caps(self._resize(self.k_msg, job[2], self.cap_msg))
         self.rounds += rounds
-        return rounds
+        self.last_rounds = rounds
+
+    def sim_env(self, global_env: int):
+        """(Batch, local index) of a job env this rank simulates, else None."""
+        le = int(global_env) - self.env_base
+        return (self.batch, le) if 0 <= le < self.E else None
 
     # ---- owned Q blocks (assembled over ranks by the caller) --------------------------------------
     def owned_q(self, global_env: int):
@@ -332,3 +350,157 @@ class PartitionedBatch:
                 n = (1 << P_) * cm.K * 3 * int(A["q_w"][g])
                 mk[int(A["q_off"][g]):int(A["q_off"][g]) + n] = True
         return mk
+
+
+def cohort_sizes(E: int, cohorts: int) -> List[int]:
+    """A rank's E envs split into ``cohorts`` consecutive cohorts as evenly as possible."""
+    return [E // cohorts + (1 if c < E % cohorts else 0) for c in range(cohorts)]
+
+
+class CohortPipeline:
+    """The rank's envs as ``cohorts`` independent partitioned jobs whose rounds overlap.
+
+    A round's phases depend on one another (local step -> message exchange -> owner step -> reply exchange
+    -> next local step), so within one job the exchanges and the small compaction / owner kernels leave the
+    GPU waiting, and the local step's last waves run with the chip mostly idle.  The envs are independent
+    (an env's records touch only that env's rows), so splitting them into cohorts -- each a PartitionedBatch
+    of its own, with its own message segments, owned-row table, stream and process group (its collectives
+    never queue behind another cohort's) -- and issuing the cohorts' rounds alternately lets one cohort's
+    exchange and owner step run beside another's local step.  Every env still performs the fused run's
+    operations in order, so the results are those of one PartitionedBatch over the same envs (tests).
+
+    Job env numbering: rank r's envs are [env_base, env_base + E) as for PartitionedBatch; the rank's
+    cohort c holds its envs [off_c, off_c + E_c) (``cohort_sizes``), and cohort c's job numbers them after
+    the lower ranks' cohort-c envs."""
+
+    def __init__(self, cm: CompiledMap, hp: dict, seeds: Sequence[int], env_base: int, envs_total: int,
+                 cohorts: int = 2, rank: int = 0, world: int = 1, dist=None, buffer_device: str = "cuda", **kw):
+        import torch
+        self.torch = torch
+        E, C_ = len(seeds), int(cohorts)
+        if C_ < 1 or E < C_:
+            raise ValueError(f"CohortPipeline: {E} envs cannot form {C_} cohorts")
+        self.cm, self.rank, self.world, self.dist = cm, int(rank), int(world), dist
+        self.E, self.env_base, self.envs_total, self.cohorts = E, int(env_base), int(envs_total), C_
+        # every rank's env count (its cohorts' sizes follow from it)
+        if dist is None or self.world == 1:
+            counts = [E]
+        else:
+            dev = "cuda" if (buffer_device == "cuda" and dist.get_backend() != "gloo") else "cpu"
+            t = torch.zeros(self.world, dtype=torch.int64, device=dev)
+            t[self.rank] = E
+            dist.all_reduce(t)
+            counts = [int(x) for x in t.cpu().tolist()]
+        if sum(counts[:self.rank]) != self.env_base or sum(counts) != self.envs_total:
+            raise ValueError(f"CohortPipeline: env_base={env_base} / envs_total={envs_total} do not match the "
+                             f"ranks' env counts {counts}")
+        self.rank_base = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
+        self.split = [cohort_sizes(n, C_) for n in counts]          # [rank][cohort] sizes
+        # one process group per cohort (created in the same order on every rank), so a cohort's collectives
+        # run on a communicator of their own
+        groups = [None] * C_
+        if dist is not None and self.world > 1 and C_ > 1:
+            groups = [dist.new_group(list(range(self.world))) for _ in range(C_)]
+        self.parts: List[PartitionedBatch] = []
+        off = 0
+        for c in range(C_):
+            n = self.split[self.rank][c]
+            base_c = sum(self.split[r][c] for r in range(self.rank))
+            tot_c = sum(self.split[r][c] for r in range(self.world))
+            self.parts.append(PartitionedBatch(cm, hp, list(seeds[off:off + n]), base_c, tot_c, rank=rank, world=world,
+                                               dist=dist, buffer_device=buffer_device, group=groups[c], **kw))
+            off += n
+        p0 = self.parts[0]
+        self.lib, self.owner, self.local_mask = p0.lib, p0.owner, p0.local_mask
+        self.last_rounds = 0
+        self.error_round = None
+
+    def close(self):
+        for p in self.parts:
+            p.close()
+
+    def learn_begin(self):
+        for p in self.parts:
+            p.learn_begin()
+
+    def apply_qinit(self):
+        for p in self.parts:
+            p.apply_qinit()
+
+    def step(self, decisions_per_env: int) -> int:
+        """Advance every local env by ``decisions_per_env`` decisions: the cohorts' rounds issued
+        alternately (each in its own stream); returns the most rounds any cohort took.  Collective."""
+        live = [(p, p.rounds_of_step(decisions_per_env)) for p in self.parts]
+        self.error_round = None
+        try:
+            while live:
+                nxt = []
+                for p, g in live:
+                    with p.stream_context():
+                        try:
+                            next(g)
+                            nxt.append((p, g))
+                        except StopIteration:
+                            pass
+                live = nxt
+        except _lib.SflError:
+            self.error_round = max((p.error_round or 0) for p in self.parts) or None
+            raise
+        self.last_rounds = max(p.last_rounds for p in self.parts)
+        return self.last_rounds
+
+    # ---- counters summed over the cohorts ----------------------------------------------------------
+    @property
+    def rounds(self):
+        return max(p.rounds for p in self.parts)
+
+    @property
+    def checkpoints(self):
+        return sum(p.checkpoints for p in self.parts)
+
+    @property
+    def deferrals(self):
+        return sum(p.deferrals for p in self.parts)
+
+    @property
+    def host_reads(self):
+        return sum(p.host_reads for p in self.parts)
+
+    @property
+    def k_msg(self):
+        return max(p.k_msg for p in self.parts)
+
+    @property
+    def cap_msg(self):
+        return max(p.cap_msg for p in self.parts)
+
+    def sync_count(self):
+        w = r = 0
+        for p in self.parts:
+            a, b = p.sync_count()
+            w, r = w + a, r + b
+        return w, r
+
+    # ---- job env -> (cohort, the cohort job's env) -------------------------------------------------
+    def _locate(self, global_env: int):
+        g = int(global_env)
+        r = int(np.searchsorted(self.rank_base, g, side="right")) - 1
+        if not (0 <= r < self.world) or g >= self.rank_base[r + 1]:
+            raise ValueError(f"env {g} outside the job's {self.envs_total} envs")
+        i = g - int(self.rank_base[r])
+        for c, n in enumerate(self.split[r]):
+            if i < n:
+                return r, c, sum(self.split[q][c] for q in range(r)) + i
+            i -= n
+        raise AssertionError("unreachable")
+
+    def owned_q(self, global_env: int):
+        _, c, ge = self._locate(global_env)
+        return self.parts[c].owned_q(ge)
+
+    def owned_mask(self) -> np.ndarray:
+        return self.parts[0].owned_mask()
+
+    def sim_env(self, global_env: int):
+        r, c, ge = self._locate(global_env)
+        return self.parts[c].sim_env(ge) if r == self.rank else None

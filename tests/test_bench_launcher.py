@@ -64,6 +64,22 @@ def test_gpus_4_host_rehearsal_runs_the_partitioned_leg():
     assert leg["rounds_per_step"] >= 25  # (the host build's local step sends every row: decisions + 1 rounds)
 
 
+def test_gpus_2_host_rehearsal_partition_with_cohorts():
+    """bench.py --partition --cohorts 2 on two host-build ranks over gloo: each rank's envs as two cohort jobs
+    (a process group each), owned rows and env states of the sampled envs checked against a fused host run."""
+    r = _bench(["--gpus", "2", "--rehearse-on-host", "--partition", "--cohorts", "2", "--config", "c5", "--envs", "4",
+                "--decisions", "24", "--steps", "1", "--warmup", "1", "--verify-envs", "4"], _env(OMP_NUM_THREADS="2"),
+               timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    res = json.loads(lines[0])
+    assert res["world_size"] == 2 and res["config"]["cohorts"] == 2, res
+    # (each rank checks its owned rows of the job's sampled envs: parity.spread(8, 4) = 3 envs, on 2 ranks)
+    assert res["parity"] == "ok" and res["parity_envs_checked"] == 6, res
+    assert res["config"]["rounds_per_step"] == 25  # (the host build sends every row: decisions + 1 rounds)
+
+
 def test_world_size_other_than_gpus_is_refused():
     r = _bench(["--gpus", "3", "--steps", "1"], _env(WORLD_SIZE="2", RANK="0", LOCAL_RANK="0"), timeout=60)
     assert r.returncode == 2

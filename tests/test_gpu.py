@@ -15,6 +15,7 @@ comp = importlib.import_module("network-distributed-q-learning_amd.compiler")
 runtime = importlib.import_module("network-distributed-q-learning_amd.runtime")
 _lib = importlib.import_module("network-distributed-q-learning_amd._lib")
 build = importlib.import_module("network-distributed-q-learning_amd.build")
+parity = importlib.import_module("network-distributed-q-learning_amd.parity")
 HP = dict(gamma=1.0, epsilon=0.5, epsilon_decay_rate=0.9997, lr=0.1, lr_decay_rate=1.0, default_q=0.0)
 CASES = _golden.cases()
 
@@ -243,6 +244,40 @@ def test_partitioned_rounds_gpu_equal_fused(lib, cfg, E, kernel, local_rows):
     ref.close()
 
 
+@pytest.mark.parametrize("cohorts", [2, 3])
+def test_cohort_pipeline_gpu_equal_fused(lib, cohorts):
+    """partition.CohortPipeline on the GPU, one rank: the envs as independent partitioned jobs on their own
+    streams, their rounds issued alternately (kernels of different cohorts run concurrently), block 0 of a
+    4-rank partition in place; every env's rows bit-equal to the fused kernel."""
+    import torch
+    part = importlib.import_module("network-distributed-q-learning_amd.partition")
+    cm = comp.compile_scenario(mapgen.make_config("c5"))
+    E = 200
+    seeds = [2000 + i for i in range(E)]
+    ref = runtime.Batch(cm, HP, seeds, lib=lib, ntab=1 << 14)
+    ref.learn_begin()
+    ref.apply_qinit()
+    loc = (part.partition_switches(cm, 4) == 0).astype(np.uint8)
+    pb = part.CohortPipeline(cm, HP, seeds, 0, E, cohorts=cohorts, lib=lib, ntab=1 << 14, buffer_device="cuda",
+                             local_rows=loc)
+    assert len({p.stream.cuda_stream for p in pb.parts}) == cohorts
+    pb.learn_begin()
+    pb.apply_qinit()
+    for n in (40, 300):
+        ref.step(n)
+        assert 1 < pb.step(n) <= n + 1
+    torch.cuda.synchronize()
+    for e in range(E):
+        q, t = pb.owned_q(e)
+        qr, tr = ref.q_raw(e)
+        assert np.array_equal(q, qr) and np.array_equal(t, tr), f"env {e}"
+        b, le = pb.sim_env(e)
+        for x, y in zip(parity.env_state(b, le), parity.env_state(ref, e)):
+            assert np.array_equal(np.asarray(x), np.asarray(y)), f"env {e} state"
+    pb.close()
+    ref.close()
+
+
 def test_partition_staging_overflow_reported_in_its_step(lib):
     """More update records in one env's round than its staging slots hold (upd_per_env 2, every row a
     message): the wave kernel's run raises E_MSG_OVF (flag 16) in the step where it happened -- the same step
@@ -272,6 +307,13 @@ def test_two_rank_partition_wave_gpu(lib, cfg, world):
     bit-equal to the fused run of all envs (host build)."""
     from tests import test_partition
     test_partition.two_rank_run(cfg, gpu=True, world=world)
+
+
+def test_two_rank_cohorts_gpu(lib):
+    """Two ranks on GPU 0 over gloo, two cohorts per rank (a process group and a stream each), the
+    cohorts' rounds alternating; bit-equal to the fused run (segments starting at 2 records)."""
+    from tests import test_partition
+    test_partition.two_rank_run("c5", gpu=True, world=2, steps=(90, 60), k_init=2, cohorts=2)
 
 
 def test_two_rank_partition_gpu_rounds_queue_between_checkpoints(lib):

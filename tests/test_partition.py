@@ -62,8 +62,9 @@ def _check_rank(pb, ref, local_ids):
         bits = np.unpackbits(t.view(np.uint8), bitorder="little")[:pb.cm.rows_per_env].astype(bool)
         rbits = np.unpackbits(tr.view(np.uint8), bitorder="little")[:pb.cm.rows_per_env].astype(bool)
         assert np.array_equal(bits, rbits & own_rows), ("touched", pb.rank, ge)
-    for le, ge in enumerate(local_ids):
-        a, b_ = _env_state(pb.batch, le), _env_state(ref, ge)
+    for ge in local_ids:
+        b, le = pb.sim_env(ge)
+        a, b_ = _env_state(b, le), _env_state(ref, ge)
         assert a[0] == b_[0] and a[1] == b_[1]
         for x, y in zip(a[2:], b_[2:]):
             assert np.array_equal(x, y)
@@ -79,6 +80,23 @@ def test_single_rank_partition_matches_fused(cfg):
     for n in (70, 130):
         assert pb.step(n) == n + 1
     _check_rank(pb, _fused(cm, seeds, (70, 130)), range(4))
+
+
+@pytest.mark.parametrize("cfg,cohorts", [("c2", 2), ("c5", 3)])
+def test_single_rank_cohorts_match_fused(cfg, cohorts):
+    """CohortPipeline: the envs split into independent partitioned jobs whose rounds alternate; every env's
+    rows and state are still the fused run's."""
+    cm = comp.compile_scenario(mapgen.make_config(cfg))
+    seeds = [450565 + i for i in range(5)]
+    pb = part.CohortPipeline(cm, HP, seeds, 0, 5, cohorts=cohorts, lib=hostsim.lib(), ntab=4096, buffer_device="cpu")
+    assert [p.E for p in pb.parts] == part.cohort_sizes(5, cohorts) and pb.E == 5
+    pb.learn_begin()
+    pb.apply_qinit()
+    for n in (70, 130):
+        assert pb.step(n) == n + 1
+    _check_rank(pb, _fused(cm, seeds, (70, 130)), range(5))
+    with pytest.raises(ValueError):
+        part.CohortPipeline(cm, HP, seeds[:1], 0, 1, cohorts=2, lib=hostsim.lib(), ntab=4096, buffer_device="cpu")
 
 
 def test_partition_switches_balanced_and_local():
@@ -123,7 +141,7 @@ def _check_round_log(pb, log, last):
             assert log[j] == log[j - 1], (pb.rank, j, log[j - 1], log[j])
 
 
-def _worker(rank, world, port, cfg, q, gpu=False, steps=(90, 60), k_init=None, log_rounds=False):
+def _worker(rank, world, port, cfg, q, gpu=False, steps=(90, 60), k_init=None, log_rounds=False, cohorts=1):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world), RANK=str(rank),
                           LOCAL_RANK=str(rank))
@@ -137,10 +155,15 @@ def _worker(rank, world, port, cfg, q, gpu=False, steps=(90, 60), k_init=None, l
             kw = dict(lib=lib, device=0, buffer_device="cuda")
         else:
             kw = dict(lib=hostsim.lib(), buffer_device="cpu")
-        pb = part.PartitionedBatch(cm, HP, seeds, rank * e_loc, world * e_loc, rank=rank, world=world, dist=dist,
-                                   ntab=4096, k_init=k_init, **kw)
+        if cohorts > 1:  # independent cohorts, each its own partitioned job (process group, segments, stream)
+            pb = part.CohortPipeline(cm, HP, seeds, rank * e_loc, world * e_loc, cohorts=cohorts, rank=rank,
+                                     world=world, dist=dist, ntab=4096, k_init=k_init, **kw)
+        else:
+            pb = part.PartitionedBatch(cm, HP, seeds, rank * e_loc, world * e_loc, rank=rank, world=world, dist=dist,
+                                       ntab=4096, k_init=k_init, **kw)
         if gpu:
-            assert pb.batch.counters()["kernel_variant"] > 0
+            for p in getattr(pb, "parts", [pb]):
+                assert p.batch.counters()["kernel_variant"] > 0
         pb.learn_begin()
         pb.apply_qinit()
         stats = {}
@@ -196,6 +219,13 @@ def two_rank_run(cfg, gpu=False, world=2, **kw):
 @pytest.mark.parametrize("cfg,world", [("c2", 2), ("c5", 2), ("c5", 3)])
 def test_two_rank_partition_matches_fused(cfg, world):
     two_rank_run(cfg, world=world)
+
+
+@pytest.mark.parametrize("world,k_init", [(2, None), (3, 2)])
+def test_multi_rank_cohorts_match_fused(world, k_init):
+    """Two cohorts per rank, each with its own process group: rounds alternate between the cohorts'
+    collectives on every rank, and the results stay the fused run's (with deferrals when k_init is small)."""
+    two_rank_run("c5", world=world, cohorts=2, k_init=k_init)
 
 
 def test_two_rank_1024_decision_step_syncs_only_at_checkpoints():
