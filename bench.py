@@ -522,8 +522,8 @@ def bench_partition(args):
 
 
 # --partition's default cohorts on the GPU (round 5, profiles/r05m_part_cohorts.txt: 1 / 2 / 3 / 4 cohorts
-# 98.6 / 101.1 / 103.1 / 73.4 M per GPU on the 8-rank rehearsal; 4 cohort streams and torch's own exceed the
-# process's 4 hardware queues)
+# 98.6 / 101.1 / 103.1-105.3 / 73.4 M per GPU on the 8-rank rehearsal; with more cohorts, or more hardware
+# queues than the default 4, the cohorts' local steps run fully side by side and every round finishes later)
 PARTITION_COHORTS = 3
 
 
