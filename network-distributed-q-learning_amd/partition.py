@@ -23,6 +23,10 @@ round (k_part_compact), so each exchange is a fixed-size all-to-all.  On the GPU
 torch stream, handed to the library with sfl_set_stream; RCCL collectives follow it): the host
 reads the counts only at checkpoint rounds (1, 2, 4, ..., 32, then every 32nd), where the ranks
 also agree on the next segment sizes -- no host synchronisation in the rounds between.
+
+CohortPipeline splits a rank's envs into independent cohorts -- each a PartitionedBatch with its own segments,
+stream and process group -- and issues their rounds alternately, so one cohort's exchange and owner step run
+beside another's local step (bench.py --partition --cohorts).
 """
 from __future__ import annotations
 
