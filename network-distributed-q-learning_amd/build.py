@@ -22,8 +22,12 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("SFL_ARCH", "gfx950")
-SOURCES = ["sfl.hip", "sfl_core.h", "sfl_wave.h", "sfl_rng.h", "sfl_engine.h", "sfl_part.h", "sfl_mfgen.h", "sfl_capi.inc", "sfl_hostsim.cpp",
-           "sfl_experiment.h", os.path.join("..", "..", "include", "sfl.h")]
+SOURCES = ["sfl.hip", "sfl_kwave_v7.hip", "sfl_kwave_g.h", "sfl_core.h", "sfl_wave.h", "sfl_rng.h", "sfl_engine.h", "sfl_part.h",
+           "sfl_mfgen.h", "sfl_capi.inc", "sfl_hostsim.cpp", "sfl_experiment.h", os.path.join("..", "..", "include", "sfl.h")]
+# libsfl.so's translation units and the compiler flags each adds to the common ones: variant 7 of k_wave_g (the
+# bench's c3 shape) with LLVM's register-minimising machine scheduler -- c3 +6.5 %, every other kernel loses with
+# it (round 5, profiles/r05p_sched_strategy_ab.txt).  Part of the build id (kernel_source_sha1).
+TUS = {"sfl.hip": [], "sfl_kwave_v7.hip": ["-mllvm", "-amdgpu-sched-strategy=iterative-minreg"]}
 _MARK = re.compile(rb"SFL_BUILD_ID:([0-9a-f]{40})")
 _DEFS = re.compile(rb"SFL_BUILD_DEFS:\[([^\]\x00]*)\]")
 _FLAGS = re.compile(rb"SFL_BUILD_FLAGS:\[([^\]\x00]*)\]")
@@ -38,6 +42,7 @@ def kernel_source_sha1() -> str:
     h = hashlib.sha1()
     for f in SOURCES:
         h.update(open(os.path.join(CSRC, f), "rb").read())
+    h.update(repr(sorted(TUS.items())).encode())
     return h.hexdigest()
 
 
@@ -96,14 +101,35 @@ def build_hip(force: bool = False, verbose: bool = False, out: str = None, defin
         defines.append("SFL_EXPERIMENT")
     if force or _stale(out, defines, flags):
         defs = " ".join(sorted(defines))
-        cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off",
-               "-Wno-unused-result", "-Wno-unused-value", f'-DSFL_BUILD_ID="{build_id(defines, flags)}"',
-               f'-DSFL_BUILD_DEFS="{defs}"', f'-DSFL_BUILD_FLAGS="{" ".join(flags)}"'] + \
-              [f"-D{d}" for d in defines] + list(flags) + ["-o", out + f".{os.getpid()}.tmp", os.path.join(CSRC, "sfl.hip")]
-        if verbose:
-            print(" ".join(cmd), flush=True)
-        subprocess.run(cmd, check=True, cwd=CSRC)
-        os.replace(out + f".{os.getpid()}.tmp", out)
+        common = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
+                  "-Wno-unused-result", "-Wno-unused-value", f'-DSFL_BUILD_ID="{build_id(defines, flags)}"',
+                  f'-DSFL_BUILD_DEFS="{defs}"', f'-DSFL_BUILD_FLAGS="{" ".join(flags)}"'] + \
+                 [f"-D{d}" for d in defines] + list(flags)
+        tmp = out + f".{os.getpid()}.tmp"
+        objs, procs = [], []
+        for tu, tu_flags in TUS.items():
+            # (a tuning build that picks its own scheduler strategy applies it to every unit)
+            extra = [] if any("amdgpu-sched-strategy" in f for f in flags) else tu_flags
+            obj = f"{tmp}.{os.path.splitext(tu)[0]}.o"
+            cmd = common + extra + ["-c", "-o", obj, os.path.join(CSRC, tu)]
+            if verbose:
+                print(" ".join(cmd), flush=True)
+            objs.append(obj)
+            procs.append((cmd, subprocess.Popen(cmd, cwd=CSRC)))
+        try:
+            for cmd, p in procs:
+                if p.wait() != 0:
+                    raise subprocess.CalledProcessError(p.returncode, cmd)
+            subprocess.run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs, check=True, cwd=CSRC)
+        finally:
+            for cmd, p in procs:
+                if p.poll() is None:
+                    p.kill()
+                    p.wait()
+            for o in objs:
+                if os.path.exists(o):
+                    os.remove(o)
+        os.replace(tmp, out)
     return out
 
 

@@ -15,7 +15,10 @@
 #include <string>
 
 #include "sfl_engine.h"
+#include "sfl_kwave_g.h"
 #include "sfl_wave.h"
+
+SFL_KWAVE_V7(extern template)  // (defined in sfl_kwave_v7.hip)
 
 #ifndef SFL_WAVE_OCC
 #define SFL_WAVE_OCC 6  // waves per SIMD the one-env-per-wave kernel is register-budgeted for (6: 80 VGPRs)
@@ -50,17 +53,10 @@ __global__ void __launch_bounds__(SFL_WAVE_BLOCK) __attribute__((amdgpu_waves_pe
                                               const sfl::SflCtl* __restrict__ c) {
   sfl::wave::run<PPL, SPL, TW, TRACE, false, TIMED>(*m, *s, *c);
 }
-// several envs per wavefront (sfl_wave.h run_groups): G lanes per env, SFL_WAVE_BLOCK / G envs per block
-// waves per SIMD the grouped kernel is register-budgeted for: shapes with one train slot per lane
-// (TW <= G) 4 -- c2 (variant 6): 918 M vs 805 M at 3 (VGPR-bound, spills a little; 5: 589 M) --,
-// two slots per lane 4 with the prefetch ring (SFL_PF_RING: the LDS then allows 4 blocks per CU),
-// 3 without it
-// (sfl::kVariants[v].OCC)
-template <int PPL, int SPL, int TW, bool TRACE, int G, int OCC, bool TIMED = false>
-__global__ void __launch_bounds__(SFL_GROUP_BLOCK) __attribute__((amdgpu_waves_per_eu(OCC)))
-k_wave_g(const sfl::SflMap* __restrict__ m, const sfl::SflState* __restrict__ s, const sfl::SflCtl* __restrict__ c) {
-  sfl::wave::run_groups<PPL, SPL, TW, TRACE, G, TIMED>(*m, *s, *c);
-}
+// several envs per wavefront: k_wave_g (sfl_kwave_g.h).  Variant 7 -- the bench's c3 shape -- is compiled in
+// its own translation unit (sfl_kwave_v7.hip) with another register-allocation-aware scheduler; this one
+// only declares it (below the includes).
+using sflk::k_wave_g;
 // maps with 65-128 trains (two train slots per lane): one env per 64-thread block (its LDS is
 // ~22 KB), register budget for the LDS-bound occupancy of 2 waves per SIMD
 #ifndef SFL_WAVE2_OCC
@@ -605,6 +601,11 @@ struct HipBackend {
   void print_prof() {
       unsigned long long pr[32] = {};
       hipMemcpyFromSymbol(pr, HIP_SYMBOL(sfl::wave::g_prof), sizeof pr);
+      {  // variant 7's kernels count into their own translation unit's copy
+        unsigned long long p7[32] = {};
+        sflk::kwave_v7_prof_take(p7);
+        for (int k = 0; k < 32; ++k) pr[k] += p7[k];
+      }
       fprintf(stderr,
               "[sfl profile] cycles reset %.3e tick %.3e decide %.3e (observe %.3e egreedy %.3e apply %.3e) post %.3e "
               "total %.3e | prefetch %llu row hit %llu miss %llu pend hit %llu miss %llu decisions %llu\n",

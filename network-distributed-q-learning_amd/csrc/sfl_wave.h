@@ -46,7 +46,7 @@ namespace wave {
 #ifdef SFL_PROFILE
 // tuning builds only: wall cycles per phase summed over waves (reset, tick, decide, post, total,
 // decide = observe + egreedy + apply)
-__device__ unsigned long long g_prof[32];
+static __device__ unsigned long long g_prof[32];  // (one per translation unit: sfl_kwave_v7.hip has its own)
 #define SFL_PCNT(k) (prof[k] += 1)
 #define SFL_LAP0() (lap_t = (uint64_t)__builtin_amdgcn_s_memtime())
 #define SFL_LAP(k)                                                 \
