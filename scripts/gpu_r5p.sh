@@ -1,11 +1,12 @@
 # round 5, call P: LLVM AMDGPU scheduler strategies (whole-library -mllvm -amdgpu-sched-strategy=...) on every
-# bench workload: c2 at 4,096 and 65,536 envs, c5 fused at 16,384 envs, and the 8-rank partition rehearsal.
+# bench workload: (C3=1: c3,) c2 at 4,096 and 65,536 envs, c5 fused at 16,384 envs, and the 8-rank partition rehearsal.
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 OUT=gpurun_out/${TAG:-r5p}
 mkdir -p $OUT
 L3="${LIBS:-libsfl libsfl_minreg libsfl_mmc libsfl}"
+[ -n "$C3" ] && { TAG=${TAG:-r5p}/c3 STEPS=ab LIBS="$L3" BSTEPS=6 bash scripts/gpu_r4.sh || exit 1; }
 TAG=${TAG:-r5p}/c2_4096 STEPS=ab LIBS="$L3" BSTEPS=10 BENCH_ARGS="--config c2 --envs 4096" bash scripts/gpu_r4.sh || exit 1
 TAG=${TAG:-r5p}/c2_65536 STEPS=ab LIBS="$L3" BSTEPS=6 BENCH_ARGS="--config c2 --envs 65536" bash scripts/gpu_r4.sh || exit 1
 TAG=${TAG:-r5p}/c5_16384 STEPS=ab LIBS="$L3" BSTEPS=4 BENCH_ARGS="--config c5 --envs 16384" bash scripts/gpu_r4.sh || exit 1

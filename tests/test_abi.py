@@ -123,6 +123,16 @@ def test_build_id_covers_defines():
     assert build.build_id(["B", "A"]) == build.build_id(["A", "B"])
 
 
+def test_build_id_covers_the_translation_units_flags(monkeypatch):
+    """libsfl.so is linked from build.TUS (c3's kernel in its own unit with its own scheduler flags): a change of
+    a unit's flags is a different build."""
+    assert "sfl.hip" in build.TUS and all(os.path.exists(os.path.join(build.CSRC, tu)) for tu in build.TUS)
+    assert all(tu in build.SOURCES for tu in build.TUS)
+    base = build.kernel_source_sha1()
+    monkeypatch.setitem(build.TUS, "sfl_kwave_v7.hip", [])
+    assert build.kernel_source_sha1() != base
+
+
 def test_product_library_carries_no_defines():
     path = build.build_hip()
     assert build.built_id(path) == build.product_build_id()
