@@ -19,6 +19,7 @@ import argparse
 import glob
 import importlib
 import json
+import math
 import os
 import socket
 import subprocess
@@ -332,6 +333,9 @@ def main():
     ap.add_argument("--envs", type=int, default=65536, help="envs per GPU")
     ap.add_argument("--config", default="c3")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--sustain-seconds", type=float, default=8.0,
+                    help="after the parity check, repeat the step for about this long and report the rate as "
+                         "'sustained' (0: skip)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--verify-envs", type=int, default=32,
                     help="envs per rank re-run on the host build after timing and compared bit-exactly (0: none)")
@@ -431,6 +435,22 @@ def main():
     if args.verify_envs > 0:
         checked, bad = verify_fused(b, cm, seeds, [args.decisions] * (args.warmup + args.steps), args.verify_envs)
     pfield = parity_field(dist, checked, bad, device=red_dev)
+    # after the parity check: the same step repeated for about --sustain-seconds, timed the same way (barrier +
+    # synchronize on both sides, max over ranks) -- the rate over a longer window than the K timed steps, so that
+    # a sampler of the GPU's activity around the run sees the kernel running
+    sustained = None
+    if args.sustain_seconds > 0 and not host and args.steps > 0:
+        n_sus = max(1, int(math.ceil(args.sustain_seconds / max(1e-6, dt / args.steps))))
+        barrier()
+        t1 = time.perf_counter()
+        tot_s = 0
+        for _ in range(n_sus):
+            tot_s += b.step(args.decisions)[0]
+        barrier()
+        dt_s, tot_s_all = par.reduce_timing(dist, time.perf_counter() - t1, float(tot_s), device=red_dev)
+        sustained = {"value": tot_s_all / dt_s, "steps": n_sus, "seconds": dt_s,
+                     "what": "the same step repeated after the parity check (not the timed K steps): the rate over a "
+                             "longer window"}
     res = None
     if rank == 0:
         avg_ms = kms / max(1, args.steps)
@@ -468,6 +488,7 @@ def main():
             "backend": (dist.get_backend() if dist is not None else None),
             "devices": devices,
             **pfield,
+            "sustained": sustained,
         }
         if host:
             res["rehearsal"] = ("--rehearse-on-host: every rank ran the host build of the kernel body; a launcher "
