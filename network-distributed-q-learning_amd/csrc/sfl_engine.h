@@ -113,8 +113,11 @@ struct Handle {
 struct WaveShape {
   int PPL, SPL, TW, G, OCC;
 };
+#ifndef SFL_V7_OCC
+#define SFL_V7_OCC 4  // variant 7 (c3): waves per SIMD its registers are budgeted for (tuning builds: 3)
+#endif
 constexpr WaveShape kVariants[] = {{0, 0, 0, 64, 0},    {1, 1, 32, 64, 0},  {4, 1, 32, 64, 0}, {4, 1, 64, 64, 0},
-                                   {8, 2, 64, 64, 0},   {16, 4, 128, 64, 0}, {4, 1, 16, 16, 4}, {16, 4, 32, 16, 4},
+                                   {8, 2, 64, 64, 0},   {16, 4, 128, 64, 0}, {4, 1, 16, 16, 4}, {16, 4, 32, 16, SFL_V7_OCC},
                                    {2, 1, 32, 32, 4},   {8, 2, 32, 32, 4},   {8, 2, 8, 8, SFL_G8_OCC1}};
 constexpr int kNumVariants = 11;
 #ifndef SFL_DEFAULT_G
