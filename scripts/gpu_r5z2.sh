@@ -7,10 +7,10 @@ OUT=gpurun_out/${TAG:-r5z}
 mkdir -p $OUT
 B="--config c2 --envs 4096"
 timeout -k 10 300 python bench.py $B --steps 10 --warmup 2 --no-cpu > $OUT/c2_bench.json 2> $OUT/c2_bench.err; rc=$?; echo "c2 bench rc=$rc"; [ $rc -eq 0 ] || { tail -5 $OUT/c2_bench.err; exit $rc; }
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/c2_prof -o ktrace --output-format csv -- python bench.py $B --steps 10 --warmup 2 --no-cpu --verify-envs 0 > /dev/null 2>&1; rc=$?; echo "c2 ktrace rc=$rc"; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/c2_prof -o ktrace --output-format csv -- python bench.py $B --steps 10 --warmup 2 --no-cpu --sustain-seconds 0 --verify-envs 0 > /dev/null 2>&1; rc=$?; echo "c2 ktrace rc=$rc"; [ $rc -eq 0 ] || exit $rc
 for C in FETCH_SIZE WRITE_SIZE "TCC_HIT_sum TCC_MISS_sum"; do
   N=$(echo $C | tr ' ' '_')
-  timeout -s KILL 240 rocprofv3 --pmc $C --kernel-trace -d $OUT/c2/pmc_$N -o pmc --output-format csv -- python bench.py $B --steps 3 --warmup 1 --no-cpu --verify-envs 0 > /dev/null 2>&1; rc=$?; echo "c2 pmc $N rc=$rc"; [ $rc -eq 0 ] || exit $rc
+  timeout -s KILL 240 rocprofv3 --pmc $C --kernel-trace -d $OUT/c2/pmc_$N -o pmc --output-format csv -- python bench.py $B --steps 3 --warmup 1 --no-cpu --sustain-seconds 0 --verify-envs 0 > /dev/null 2>&1; rc=$?; echo "c2 pmc $N rc=$rc"; [ $rc -eq 0 ] || exit $rc
 done
 TAG=${TAG:-r5z}/c2 BENCH_ARGS="$B --verify-envs 0" DEC=$((4096*1024)) bash scripts/gpu_waitsplit.sh || exit 1
 timeout -k 10 300 python bench.py --config c2 --steps 10 --warmup 2 --no-cpu > $OUT/c2_65536_bench.json 2> $OUT/c2_65536.err; rc=$?; echo "c2 65536 rc=$rc"; [ $rc -eq 0 ] || exit $rc

@@ -15,7 +15,7 @@ for C in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT
          LdsLatency VmemLatency SmemLatency \
          "SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SMEM SQ_INSTS_BRANCH SQ_WAVES SQ_BUSY_CYCLES SQ_INST_CYCLES_VMEM_RD SQ_INST_CYCLES_VMEM_WR" ${EXTRA_PMC}; do
   i=$((i+1))
-  timeout -s KILL 180 rocprofv3 --pmc $C --kernel-trace -d $OUT/ws_$i -o pmc --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu ${BENCH_ARGS} > $OUT/ws_$i.json 2>$OUT/ws_$i.err
+  timeout -s KILL 180 rocprofv3 --pmc $C --kernel-trace -d $OUT/ws_$i -o pmc --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu --sustain-seconds 0 ${BENCH_ARGS} > $OUT/ws_$i.json 2>$OUT/ws_$i.err
   rc=$?; echo "pmc $i ($C) rc=$rc"; [ $rc -eq 0 ] || exit $rc
 done
 python scripts/pmc_per_dec.py "$OUT/ws_*" ${DEC} > $OUT/per_dec.txt; cat $OUT/per_dec.txt
