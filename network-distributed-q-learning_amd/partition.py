@@ -133,6 +133,7 @@ class PartitionedBatch:
         self.on_gpu = dev.type == "cuda"
         self.rec = (ms.value, rp.value)
         self.rounds = 0
+        self.last_rounds = 0  # rounds of the last completed step
         self._counts = (C.c_uint32 * (2 * self.world + 3))()   # sfl_part_counts, sfl_part.h PART_C_*
         self.k_msg = self.cap_msg
         self.host_reads = 0   # checkpoint reads of the counts (the host's only look at a round's results)
