@@ -352,7 +352,7 @@ def main():
     ap.add_argument("--cohorts", type=int, default=None,
                     help="--partition: the rank's envs as this many independent partitioned jobs whose rounds are "
                          "issued alternately (partition.CohortPipeline), so one cohort's exchange and owner step "
-                         "overlap another's local step (default: %d on the GPU, 1 on the host build)" % 3)
+                         "overlap another's local step (default: %d on the GPU, 1 on the host build)" % PARTITION_COHORTS)
     ap.add_argument("--partition", action="store_true",
                     help="graph-partitioned mode (BASELINE configs[4]): switch agents owned by ranks, RCCL all-to-all "
                          "of row lookups and updates; defaults to --config c5 --envs 16384 (238 GB of owned Q rows per GPU)")
