@@ -406,6 +406,7 @@ class CohortPipeline:
         groups = [None] * C_
         if dist is not None and self.world > 1 and C_ > 1:
             groups = [dist.new_group(list(range(self.world))) for _ in range(C_)]
+        self._groups = [g for g in groups if g is not None]
         self.parts: List[PartitionedBatch] = []
         off = 0
         for c in range(C_):
@@ -423,6 +424,9 @@ class CohortPipeline:
     def close(self):
         for p in self.parts:
             p.close()
+        for g in self._groups:  # (collective: every rank closes its pipeline)
+            self.dist.destroy_process_group(g)
+        self._groups = []
 
     def learn_begin(self):
         for p in self.parts:

@@ -191,6 +191,7 @@ def _worker(rank, world, port, cfg, q, gpu=False, steps=(90, 60), k_init=None, l
         bad = parity.check_partition(pb, HP, pick, lambda g: 450565 + g, steps, hostsim.lib(), ntab=4096)
         f = bench.parity_field(dist, len(pick), bad)
         assert f["parity"] == "ok" and f["parity_envs_checked"] == world * len(pick), f
+        pb.close()  # (a CohortPipeline also releases its cohorts' process groups)
         dist.barrier()
         dist.destroy_process_group()
         q.put((rank, "ok", stats))
