@@ -65,6 +65,29 @@ static __device__ unsigned long long g_prof[32];  // (one per translation unit: 
 #define SFL_LAP(k)
 #endif
 
+// Wave priorities (s_setprio: the SIMD's issue arbiter prefers higher-priority waves): a wave in a tick above one
+// in a decision above one in its post step / bookkeeping.  Round 5 (profiles/r05ag_wave_priority_ab.txt): tick 2,
+// decide 1 -- c3 +2.1 %, c2 at 4,096 envs +3.8 %, c2 at 65,536 envs +4.1 %, c5 fused +1.3 %; the tick must rank above
+// the decision (equal priorities lose the gain); the prefetch's own priority adds nothing; the partitioned local
+// step keeps the default priority (-1 % with them).
+#ifndef SFL_SETPRIO_PF
+#define SFL_SETPRIO_PF 0  // while the batch prefetch issues its loads (0: the caller's)
+#endif
+#ifndef SFL_SETPRIO_TICK
+#define SFL_SETPRIO_TICK 2  // during a tick (0: unchanged)
+#endif
+#ifndef SFL_SETPRIO_DECIDE
+#define SFL_SETPRIO_DECIDE 1  // during a decision (0: unchanged)
+#endif
+template <int P>
+struct PrioGuard {  // s_setprio P for the scope (P = 0: nothing)
+  __device__ __forceinline__ PrioGuard() {
+    if constexpr (P > 0) __builtin_amdgcn_s_setprio(P);
+  }
+  __device__ __forceinline__ ~PrioGuard() {
+    if constexpr (P > 0) __builtin_amdgcn_s_setprio(0);
+  }
+};
 constexpr uint32_t PF_NONE = 0xFFFFFFFFu;
 // batch-prefetch record per train: doubles -- the pending cell, the slot word, the staged row's max;
 // words -- distance-map values at the train's cell (observation), at its projected cell if it stops
@@ -1115,6 +1138,7 @@ struct WEnv {
   // ---- one Flatland tick + switchfl bookkeeping (switch_env.py:296-401, 427-485;
   //      flatland_lite.RailEnv.step), train-parallel: lane h = train h ----------------------------
   __device__ __forceinline__ void tick() {
+    PrioGuard<PART ? 0 : SFL_SETPRIO_TICK> prio;  // (the partitioned local step: no gain, profiles/r05ag_*)
     SFL_LAP0();
     if constexpr (xp::kNoTick) {
       ++now;
@@ -1457,6 +1481,7 @@ struct WEnv {
   // Q values are dropped when the batch writes their cell (pf_written).  Slot words are never
   // stale: a decision writes only its own train's slots and a train decides once per batch.
   __device__ __forceinline__ void prefetch(bool greedy) {
+    PrioGuard<PART ? 0 : SFL_SETPRIO_PF> prio;
     const Mask malf = malf_mask();
 #pragma unroll
     for (int k = 0; k < PFS; ++k) pf_roff[k] = pf_qoff[k] = PF_NONE;
@@ -1690,6 +1715,7 @@ struct WEnv {
   // applies the reply)
   template <bool TM = false>
   __device__ __forceinline__ bool decide(Dec& d, bool greedy) {
+    PrioGuard<PART ? 0 : SFL_SETPRIO_DECIDE> prio;
     // PART: a row of this rank's own switches is decided in one pass, like the fused kernel
     const bool loc = local_sw((int)(trl(sdec, mctz(q_mask)) >> 16));
     const bool observe_only = PART && !(flags & F_REQ) && !loc;
