@@ -124,11 +124,74 @@ def oracle_cores() -> int:
     return max(1, min(cores, int(quota)) if quota else cores)
 
 
+def _oracle_loop(jobs, results):
+    """A fixed oracle worker: one job from `jobs`, its result (or the error) to `results`, then exit."""
+    job = jobs.get()
+    if job is None:
+        return
+    try:
+        results.put(("ok", job[1], _oracle_worker(job)))
+    except BaseException as ex:  # noqa: BLE001 -- reported on the line
+        results.put(("error", job[1], repr(ex)))
+
+
+class OraclePool:
+    """The oracle baseline's worker processes: a FIXED set, started BEFORE any HIP call of this process (a process
+    that has initialised the GPU must not start programs: spawn = fork + exec).  Nothing ever replaces a worker --
+    unlike multiprocessing.Pool, whose handler thread respawns a dead worker (a fork + exec from a GPU-initialised
+    process) and whose map() waits forever for a lost task.  A worker that dies makes `map` raise."""
+
+    def __init__(self, n: int):
+        import multiprocessing as mp
+        ctx = mp.get_context("spawn")
+        self.jobs, self.results = ctx.Queue(), ctx.Queue()
+        self.procs = [ctx.Process(target=_oracle_loop, args=(self.jobs, self.results), daemon=True) for _ in range(n)]
+        for p in self.procs:
+            p.start()
+        self._processes = n
+        self.used = False
+
+    def map(self, jobs, timeout: float):
+        import queue
+        assert not self.used and len(jobs) <= len(self.procs)
+        self.used = True
+        for j in jobs:
+            self.jobs.put(j)
+        for _ in range(len(self.procs) - len(jobs)):
+            self.jobs.put(None)
+        out, deadline = {}, time.monotonic() + timeout
+        while len(out) < len(jobs):
+            try:
+                kind, seed, r = self.results.get(timeout=1.0)
+            except queue.Empty:
+                if time.monotonic() > deadline:
+                    raise RuntimeError(f"oracle baseline: no result from {len(jobs) - len(out)} worker(s) in {timeout:.0f} s")
+                if any(p.exitcode not in (None, 0) for p in self.procs):
+                    raise RuntimeError("oracle baseline: a worker process died without a result "
+                                       f"(exit codes {[p.exitcode for p in self.procs]})")
+                continue
+            if kind != "ok":
+                raise RuntimeError(f"oracle baseline: worker for seed {seed} failed: {r}")
+            out[seed] = r
+        return [out[j[1]] for j in jobs]
+
+    def close(self):
+        if not self.used:
+            for _ in self.procs:
+                self.jobs.put(None)
+            self.used = True
+        for p in self.procs:
+            p.join(timeout=30)
+            if p.exitcode is None:
+                p.kill()
+                p.join(timeout=5)
+
+    def join(self):
+        pass
+
+
 def start_oracle_pool(n: int):
-    """The oracle baseline's worker processes, started BEFORE any HIP call of this process (a process that has
-    initialised the GPU must not start programs: spawn = fork + exec)."""
-    import multiprocessing as mp
-    return mp.get_context("spawn").Pool(n)
+    return OraclePool(n)
 
 
 def cpu_oracle_baseline(config: str, seconds: float, pool=None, check=None):
@@ -140,7 +203,7 @@ def cpu_oracle_baseline(config: str, seconds: float, pool=None, check=None):
     Q-table must equal the oracle's (the reference's q_table dict) -- the bench line's own oracle parity on
     exactly the sample it timed."""
     jobs = [(config, 450565 + i, seconds, i == 0) for i in range(pool._processes if pool is not None else 1)]
-    res = pool.map(_oracle_worker, jobs) if pool is not None else [_oracle_worker(jobs[0])]
+    res = pool.map(jobs, timeout=4 * seconds + 120) if pool is not None else [_oracle_worker(jobs[0])]
     n_all = sum(r[0] for r in res)
     dt_max = max(r[1] for r in res)
     n0, dt0, q0 = res[0]
@@ -298,19 +361,37 @@ def issue_bound(prof):
     return out or None
 
 
-def verify_fused(b, cm, seeds, schedule, n_envs: int):
-    """Parity of a spread sample of this rank's envs vs the host build of the kernel body (after timing)."""
+def verify_threads() -> int:
+    """OpenMP threads of this rank's host-build parity check: the granted cores (cgroup quota, else the affinity
+    set) shared by the ranks of this node.  Without it libgomp starts one thread per affinity core -- 256 on the
+    GPU box, whose quota is 16 cores -- in every rank."""
+    cores, quota = host_cores()
+    granted = max(1, min(cores, int(quota)) if quota else cores)
+    return max(1, granted // max(1, int(os.environ.get("LOCAL_WORLD_SIZE", "1"))))
+
+
+def host_verifier():
+    """The host build of the kernel body, with verify_threads() OpenMP threads: (Lib, threads)."""
+    import ctypes
     build = importlib.import_module(PKG + ".build")
     _lib = importlib.import_module(PKG + "._lib")
-    parity = importlib.import_module(PKG + ".parity")
     host = _lib.Lib(build.build_hostsim())
     host.check_fresh()
+    host.dll.sflh_set_threads.restype = ctypes.c_int
+    return host, int(host.dll.sflh_set_threads(ctypes.c_int(verify_threads())))
+
+
+def verify_fused(b, cm, seeds, schedule, n_envs: int):
+    """Parity of a spread sample of this rank's envs vs the host build of the kernel body (after timing):
+    (envs checked, mismatches, OpenMP threads used)."""
+    parity = importlib.import_module(PKG + ".parity")
+    host, threads = host_verifier()
     pick = parity.spread(len(seeds), n_envs)
     bad = parity.check_batch(b, HP, pick, schedule, host)
-    return len(pick), bad
+    return len(pick), bad, threads
 
 
-def parity_field(dist, n_checked: int, bad, device=None):
+def parity_field(dist, n_checked: int, bad, device=None, threads: int = 0):
     """Job-wide parity verdict: envs checked and mismatches summed over ranks."""
     par = importlib.import_module(PKG + ".parallel")
     _, n_all = par.reduce_timing(dist, 0.0, float(n_checked), device=device)
@@ -320,7 +401,9 @@ def parity_field(dist, n_checked: int, bad, device=None):
             "parity_envs_checked": int(n_all),
             "parity_reference": "libsfl_hostsim.so (the kernel body built for the host, pinned to the oracle and "
                                 "the reference's golden traces by tests/), same seeds and step schedule, "
-                                "Q-table + key set + env state bit-exact",
+                                f"Q-table + key set + env state bit-exact; {threads} OpenMP thread(s) per rank "
+                                "(the granted host cores / the ranks of the node)",
+            "parity_threads_per_rank": threads,
             "parity_first_mismatches": list(bad[:4])}
 
 
@@ -352,7 +435,8 @@ def main():
     ap.add_argument("--cohorts", type=int, default=None,
                     help="--partition: the rank's envs as this many independent partitioned jobs whose rounds are "
                          "issued alternately (partition.CohortPipeline), so one cohort's exchange and owner step "
-                         "overlap another's local step (default: %d on the GPU, 1 on the host build)" % PARTITION_COHORTS)
+                         "overlap another's local step (default: %d on one GPU; 1 on the host build and with RCCL at N > 1)"
+                         % PARTITION_COHORTS)
     ap.add_argument("--partition", action="store_true",
                     help="graph-partitioned mode (BASELINE configs[4]): switch agents owned by ranks, RCCL all-to-all "
                          "of row lookups and updates; defaults to --config c5 --envs 16384 (238 GB of owned Q rows per GPU)")
@@ -395,9 +479,7 @@ def main():
     seeds = par.shard_seeds(450565, E, rank)
     lib = None
     if host:
-        _lib = importlib.import_module(PKG + "._lib")
-        lib = _lib.Lib(build.build_hostsim())
-        lib.check_fresh()
+        lib, _ = host_verifier()  # (its OpenMP threads bounded like the parity check's)
     b = runtime.Batch(cm, HP, seeds, device=dev, lib=lib)
     b.learn_begin()
     b.apply_qinit()
@@ -431,10 +513,11 @@ def main():
     dt = time.perf_counter() - t0
     dt, total_all = par.reduce_timing(dist, dt, float(total), device=red_dev)
     # after the timed region: a spread sample of every rank's envs re-run on the host build, bit-exact
-    checked, bad = 0, ["not verified (--verify-envs 0)"]
+    checked, bad, vthreads = 0, ["not verified (--verify-envs 0)"], 0
     if args.verify_envs > 0:
-        checked, bad = verify_fused(b, cm, seeds, [args.decisions] * (args.warmup + args.steps), args.verify_envs)
-    pfield = parity_field(dist, checked, bad, device=red_dev)
+        checked, bad, vthreads = verify_fused(b, cm, seeds, [args.decisions] * (args.warmup + args.steps),
+                                              args.verify_envs)
+    pfield = parity_field(dist, checked, bad, device=red_dev, threads=vthreads)
     # after the parity check: the same step repeated for about --sustain-seconds, timed the same way (barrier +
     # synchronize on both sides, max over ranks) -- the rate over a longer window than the K timed steps, so that
     # a sampler of the GPU's activity around the run sees the kernel running
@@ -496,11 +579,13 @@ def main():
             res["roofline"] = None
         if world == 1 and not args.no_cpu and not host:
             res["cpu_baseline"] = cpu_baseline(cm, args.cpu_seconds, args.config)
-            res["cpu_oracle_baseline"] = cpu_oracle_baseline(args.config, args.cpu_seconds / 2, pool=pool,
-                                                             check=(cm, dev, cnt0["group_lanes"]))
+            try:
+                res["cpu_oracle_baseline"] = cpu_oracle_baseline(args.config, args.cpu_seconds / 2, pool=pool,
+                                                                 check=(cm, dev, cnt0["group_lanes"]))
+            except RuntimeError as ex:  # a lost worker: the baseline failed, never replaced or retried
+                res["cpu_oracle_baseline"] = {"error": str(ex)}
     if pool is not None:
         pool.close()
-        pool.join()
     b.close()
     printed = []
 
@@ -564,11 +649,38 @@ def partition_run(args, par, dist, world, rank, dev, red_dev, devices, host: boo
         local = (part.partition_switches(cm, args.virtual_ranks) == 0).astype(np.uint8)
     lib = None
     if host:
-        _lib = importlib.import_module(PKG + "._lib")
-        lib = _lib.Lib(importlib.import_module(PKG + ".build").build_hostsim())
-        lib.check_fresh()
+        lib, _ = host_verifier()
     cohorts = getattr(args, "cohorts", None)
-    cohorts = min(E, cohorts if cohorts else (1 if host else PARTITION_COHORTS))
+    # default: one cohort on the host build and on an RCCL job of several ranks (each cohort has its own
+    # communicator, and concurrent communicators on one device have not been run on RCCL yet); --cohorts N asks
+    # for the pipeline anyway
+    rccl_multi = world > 1 and dist is not None and dist.get_backend() == "nccl"
+    cohorts = min(E, cohorts if cohorts else (1 if (host or rccl_multi) else PARTITION_COHORTS))
+    # the break-even comparison: the same envs run env-sharded on the fused kernel -- every rank its
+    # own envs with all their Q rows, no exchange -- timed the same way, before the partitioned job allocates
+    fused = None
+    if getattr(args, "compare_fused", True):
+        runtime = importlib.import_module(PKG + ".runtime")
+        fb = runtime.Batch(cm, HP, seeds, device=dev, lib=lib)
+        fb.learn_begin()
+        fb.apply_qinit()
+        for _ in range(args.warmup):
+            fb.step(args.decisions)
+        if dist is not None:
+            dist.barrier()
+        if not host:
+            torch.cuda.synchronize()
+        tf = time.perf_counter()
+        nf = 0
+        for _ in range(args.steps):
+            nf += fb.step(args.decisions)[0]
+        if dist is not None:
+            dist.barrier()
+        if not host:
+            torch.cuda.synchronize()
+        dtf, nf_all = par.reduce_timing(dist, time.perf_counter() - tf, float(nf), device=red_dev)
+        fused = nf_all / dtf
+        fb.close()
     kw = dict(rank=rank, world=world, dist=dist, device=dev, lib=lib, buffer_device="cpu" if host else "cuda",
               local_rows=local)
     pb = (part.CohortPipeline(cm, HP, seeds, rank * E, world * E, cohorts=cohorts, **kw) if cohorts > 1
@@ -597,18 +709,15 @@ def partition_run(args, par, dist, world, rank, dev, red_dev, devices, host: boo
     dt, total_all = par.reduce_timing(dist, dt, total, device=red_dev)
     # after the timed region: a spread sample of the job's envs, this rank's owned rows of them and the
     # state of those it simulates, vs a fused single-process host run of their seeds
-    checked, bad = 0, ["not verified (--verify-envs 0)"]
+    checked, bad, vthreads = 0, ["not verified (--verify-envs 0)"], 0
     if args.verify_envs > 0:
-        build = importlib.import_module(PKG + ".build")
-        _lib = importlib.import_module(PKG + "._lib")
         parity = importlib.import_module(PKG + ".parity")
-        host = _lib.Lib(build.build_hostsim())
-        host.check_fresh()
+        hlib, vthreads = host_verifier()
         pick = parity.spread(world * E, args.verify_envs)
         bad = parity.check_partition(pb, HP, pick, lambda g: 450565 + g, [args.decisions] * (args.warmup + args.steps),
-                                     host)
+                                     hlib)
         checked = len(pick)
-    pfield = parity_field(dist, checked, bad, device=red_dev)
+    pfield = parity_field(dist, checked, bad, device=red_dev, threads=vthreads)
     res = None
     if rank == 0:
         res = {
@@ -650,6 +759,14 @@ def partition_run(args, par, dist, world, rank, dev, red_dev, devices, host: boo
             "devices": devices,
             **pfield,
         }
+        if fused is not None:
+            # > 1 only if the partition beats running the same envs env-sharded (each GPU all Q rows of its own
+            # envs); it cannot while one env's rows fit a GPU (break-even)
+            res["env_sharded_fused"] = {"value": fused, "unit": "agent-env-steps/sec",
+                                        "what": f"the same {E} envs per GPU on the fused kernel, env-sharded over "
+                                                f"{world} rank(s) (no exchange), {args.steps} x {args.decisions} "
+                                                "decisions per env, timed the same way"}
+            res["vs_env_sharded_fused"] = res["value"] / fused if fused > 0 else None
         if host:
             res["rehearsal"] = "host build of the kernel body over gloo: a rehearsal, not a GPU measurement"
     pb.close()
@@ -715,6 +832,7 @@ def partition_leg(par, dist, world, rank, dev, red_dev, devices, res, emit, host
            "count_reads_per_step": cfgd["count_reads_per_step"], "segment_records": cfgd["segment_records"],
            "collectives_per_round": cfgd.get("collectives_per_round"), "cohorts": cfgd.get("cohorts"),
            "deferrals": cfgd["deferrals"], "parity": leg.get("parity"),
+           "vs_env_sharded_fused": leg.get("vs_env_sharded_fused"),
            "parity_envs_checked": leg.get("parity_envs_checked"), "wall_s": time.perf_counter() - t0}
     if host:
         out["rehearsal"] = leg.get("rehearsal")

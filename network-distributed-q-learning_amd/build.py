@@ -88,6 +88,13 @@ def _stale(out: str, defines=(), flags=()) -> bool:
     return built_id(out) != build_id(defines, flags)
 
 
+def link_cmd(out: str, objs, flags=()):
+    """hipcc's link line of libsfl.so: the caller's extra flags go to the link too (a build with link-relevant
+    flags -- -fgpu-rdc, sanitizer, profiling or coverage flags, -Wl,... -- must link with them; its build id
+    already claims them)."""
+    return [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC"] + list(flags) + ["-o", out] + list(objs)
+
+
 def build_hip(force: bool = False, verbose: bool = False, out: str = None, defines=(), flags=()) -> str:
     """hipcc build of libsfl.so (gfx950).  ``out``/``defines``/``flags``: alternative builds for tuning,
     never into the product path (libsfl.so); an ``SFL_X_*`` / ``SFL_AB_*`` define makes an experiment
@@ -120,7 +127,7 @@ def build_hip(force: bool = False, verbose: bool = False, out: str = None, defin
             for cmd, p in procs:
                 if p.wait() != 0:
                     raise subprocess.CalledProcessError(p.returncode, cmd)
-            subprocess.run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs, check=True, cwd=CSRC)
+            subprocess.run(link_cmd(tmp, objs, flags), check=True, cwd=CSRC)
         finally:
             for cmd, p in procs:
                 if p.poll() is None:

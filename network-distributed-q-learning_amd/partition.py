@@ -383,8 +383,8 @@ class CohortPipeline:
         import torch
         self.torch = torch
         E, C_ = len(seeds), int(cohorts)
-        if C_ < 1 or E < C_:
-            raise ValueError(f"CohortPipeline: {E} envs cannot form {C_} cohorts")
+        if C_ < 1:
+            raise ValueError(f"CohortPipeline: {C_} cohorts")
         self.cm, self.rank, self.world, self.dist = cm, int(rank), int(world), dist
         self.E, self.env_base, self.envs_total, self.cohorts = E, int(env_base), int(envs_total), C_
         # every rank's env count (its cohorts' sizes follow from it)
@@ -396,6 +396,10 @@ class CohortPipeline:
             t[self.rank] = E
             dist.all_reduce(t)
             counts = [int(x) for x in t.cpu().tolist()]
+        # (checked on the job's counts, after the all-reduce, so that every rank raises, not only the one short of
+        # envs while its peers wait in the collective)
+        if min(counts) < C_:
+            raise ValueError(f"CohortPipeline: the ranks' env counts {counts} cannot each form {C_} cohorts")
         if sum(counts[:self.rank]) != self.env_base or sum(counts) != self.envs_total:
             raise ValueError(f"CohortPipeline: env_base={env_base} / envs_total={envs_total} do not match the "
                              f"ranks' env counts {counts}")

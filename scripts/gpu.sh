@@ -1,0 +1,95 @@
+# The one GPU launcher (replaces the per-round scripts/gpu_r*.sh): run the named steps in order on the gpurun box,
+# each under its own time limit, stopping at the first failure.  Outputs under gpurun_out/$TAG.
+#
+#   gpurun --timeout 1200 -- 'TAG=r6a bash scripts/gpu.sh tests smoke bench'
+#
+# Steps:
+#   tests      pytest -m gpu (PYTEST_K: a -k filter)
+#   smoke      __graft_entry__.smoke()
+#   bench      the default bench line (CPU baselines, oracle parity); BENCH_ARGS appended
+#   driver     the driver's own command: bench.py --steps 20 --warmup 5
+#   ktrace     rocprofv3 --kernel-trace --stats of a short bench (BENCH_ARGS)
+#   pmc        the HBM-traffic passes (FETCH_SIZE, WRITE_SIZE, L2 hit/miss, memory-side requests) of a short bench
+#   waitsplit  the wave-time split per decision (scripts/pmc_per_dec.py; DEC = decisions per launch)
+#   c2         configs[1] (c2 at its 4,096 envs): ktrace + traffic passes + waitsplit, THEN its bench line (so the
+#              line carries the counter profile of its own build: commit profiles/<tag>_c2_4096_pmc.json first)
+#   c2big      c2 at 65,536 envs
+#   c5fused    c5 fused at 16,384 envs
+#   part       the 8-rank partition rehearsal on one GPU (with the env-sharded fused comparison)
+#   ab         bench for each library in LIBS (SFL_LIB, --experimental for all but libsfl)
+#   eval       the published evaluation table (scripts/eval_table.py) through libsfl.so
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+OUT=gpurun_out/${TAG:-gpu}
+mkdir -p $OUT
+
+ok() { local rc=$1; shift; echo "$* rc=$rc"; [ $rc -eq 0 ] || exit $rc; }
+line() { python -c "import json,sys;d=json.load(open('$1'));r=d.get('roofline') or {};print('  %s %.1fM/s %.2f ms/step kernel %s ms frac %s parity %s' % ('$1'.split('/')[-1], d['value']/1e6, d['ms_per_step'], r.get('avg_kernel_ms'), r.get('frac'), d.get('parity')))"; }
+SHORT="--no-cpu --sustain-seconds 0 --verify-envs 0"
+
+ktrace() {  # ktrace <dir> <bench args...>
+  local d=$1; shift
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $d -o ktrace --output-format csv -- python bench.py --steps 10 --warmup 2 $SHORT "$@" > $d.json 2>/dev/null
+}
+pmc() {  # pmc <dir> <bench args...>: one --pmc pass per counter group
+  local d=$1; shift
+  for C in FETCH_SIZE WRITE_SIZE "TCC_HIT_sum TCC_MISS_sum" "TCC_EA0_RDREQ TCC_EA0_RDREQ_32B TCC_EA0_RDREQ_64B TCC_EA0_RDREQ_128B" "TCC_EA0_RDREQ_DRAM_32B TCC_EA0_WRREQ_WRITE_DRAM_32B TCC_EA0_WRREQ_ATOMIC_DRAM_32B TCC_EA0_WRREQ"; do
+    local N=$(echo $C | tr ' ' '_' | cut -c1-40)
+    timeout -s KILL 240 rocprofv3 --pmc $C --kernel-trace -d $d/pmc_$N -o pmc --output-format csv -- python bench.py --steps 3 --warmup 1 $SHORT "$@" > /dev/null 2>&1
+    ok $? "pmc $N"
+  done
+}
+
+for S in "$@"; do
+  case $S in
+    tests)
+      timeout -k 10 1100 python -u -m pytest tests/test_gpu.py -x -v --durations=30 --timeout 300 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} > $OUT/pytest_gpu.log 2>&1
+      rc=$?; tail -3 $OUT/pytest_gpu.log; ok $rc "tests" ;;
+    smoke)
+      timeout -k 10 300 python __graft_entry__.py > $OUT/smoke.log 2>&1; rc=$?; tail -1 $OUT/smoke.log; ok $rc "smoke" ;;
+    bench)
+      timeout -k 10 600 python bench.py ${BENCH_ARGS} > $OUT/bench.json 2> $OUT/bench.err; rc=$?
+      [ $rc -eq 0 ] || tail -5 $OUT/bench.err; ok $rc "bench"; line $OUT/bench.json ;;
+    driver)
+      timeout -k 10 600 python bench.py --steps 20 --warmup 5 > $OUT/driver.json 2> $OUT/driver.err; rc=$?
+      [ $rc -eq 0 ] || tail -5 $OUT/driver.err; ok $rc "driver"; line $OUT/driver.json ;;
+    ktrace)
+      ktrace $OUT/prof ${BENCH_ARGS}; ok $? "ktrace" ;;
+    pmc)
+      pmc $OUT ${BENCH_ARGS} ;;
+    waitsplit)
+      TAG=${TAG:-gpu} bash scripts/gpu_waitsplit.sh; ok $? "waitsplit" ;;
+    c2)
+      B="--config c2 --envs 4096"
+      ktrace $OUT/c2_prof $B; ok $? "c2 ktrace"
+      pmc $OUT/c2 $B
+      TAG=${TAG:-gpu}/c2 BENCH_ARGS="$B --verify-envs 0" DEC=$((4096*1024)) bash scripts/gpu_waitsplit.sh; ok $? "c2 waitsplit"
+      timeout -k 10 300 python bench.py $B --steps 10 --warmup 2 --no-cpu > $OUT/c2_bench.json 2> $OUT/c2_bench.err; ok $? "c2 bench"
+      line $OUT/c2_bench.json ;;
+    c2big)
+      timeout -k 10 300 python bench.py --config c2 --steps 10 --warmup 2 --no-cpu > $OUT/c2_65536_bench.json 2> $OUT/c2_65536.err; ok $? "c2 65536"
+      line $OUT/c2_65536_bench.json ;;
+    c5fused)
+      timeout -k 10 300 python bench.py --config c5 --envs 16384 --steps 4 --warmup 1 --no-cpu > $OUT/c5_fused_bench.json 2> $OUT/c5_fused.err; ok $? "c5 fused"
+      line $OUT/c5_fused_bench.json ;;
+    part)
+      timeout -k 10 400 python bench.py --partition --steps 3 --warmup 1 --decisions 1024 --virtual-ranks 8 --verify-envs 4 ${PART_ARGS} > $OUT/part.json 2> $OUT/part.err; rc=$?
+      [ $rc -eq 0 ] || tail -5 $OUT/part.err; ok $rc "part"
+      line $OUT/part.json
+      python -c "import json;d=json.load(open('$OUT/part.json'));print('  fused env-sharded %.1fM/s, vs_env_sharded_fused %.3f' % (d['env_sharded_fused']['value']/1e6, d['vs_env_sharded_fused']))" ;;
+    ab)
+      for L in ${LIBS:-libsfl}; do
+        export SFL_LIB=$GRAFT_REPO_ROOT/network-distributed-q-learning_amd/$L.so
+        V="--verify-envs ${VERIFY_ENVS:-0} --experimental"; [ "$L" = "libsfl" ] && V=""
+        timeout -k 10 300 python bench.py --steps ${STEPS:-10} --warmup 2 --no-cpu $V ${BENCH_ARGS} > $OUT/ab_${L}.json 2> $OUT/ab_${L}.err; ok $? "ab $L"
+        line $OUT/ab_${L}.json
+      done
+      unset SFL_LIB ;;
+    eval)
+      timeout -k 10 900 python -u scripts/eval_table.py $OUT/eval_table.json ${EVAL_ARGS} > $OUT/eval_table.log 2>&1; rc=$?
+      tail -20 $OUT/eval_table.log; ok $rc "eval" ;;
+    *)
+      echo "unknown step $S"; exit 2 ;;
+  esac
+done

@@ -18,8 +18,9 @@ def sem_digest(semaphores) -> int:
     return zlib.crc32(repr(items).encode()) & 0xFFFFFFFF
 
 
-def replay(g, events, lib, digest_every=1):
-    """Replay one golden event list on a fresh env; returns the number of decisions checked."""
+def replay(g, events, lib, digest_every=1, max_decisions=None):
+    """Replay one golden event list on a fresh env; returns the number of decisions checked (the first
+    ``max_decisions`` of them when given: a prefix of the run)."""
     hp = g["hparams"]
     env = env_mod.ASyncSwitchEnv(g["scenario_obj"], max_steps=hp.get("max_steps", 100_000))
     seed = g["seed"]
@@ -27,7 +28,7 @@ def replay(g, events, lib, digest_every=1):
     it = None
     try:
         i = 0
-        while i < len(events):
+        while i < len(events) and (max_decisions is None or n < max_decisions):
             ev = events[i]
             if ev[0] == "R":
                 env.reset(seed=seed, lib=lib if it is None else None)

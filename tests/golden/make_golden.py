@@ -171,6 +171,10 @@ CASES = [
     # the same keys on round 4's layout: every link between neighbouring cities a rail path of its own
     # (mapgen.generate_city_grid: five cities on a 60 x 60 grid, two links per neighbouring pair, 2 or 4 tracks)
     ("citygrid_s5", ("flatland", 60, 6, 8, 2, 2), 5, (0.02, 3, 8), 2024, HP_TEST_MODEL, 10, 3),
+    # round 6: above 32 trains -- configs[4]'s map (256 switches / 128 trains: two train slots per lane, four-word
+    # train masks) and a mid-size k_wave shape (100 switches / 48 trains, the test_gpu.py variant-4 map)
+    ("c5_mf", "c5", mapgen.MAP_SEED, (0.01, 5, 15), 450565, HP_TEST_MODEL, 2, None),
+    ("grid100x48_s3", ("grid", 100, 48, 8), 4242, (0.01, 5, 15), 31337, HP_DECAY, 3, 2),
 ]
 
 
@@ -181,6 +185,8 @@ def main(only=None):
             continue
         if isinstance(cfg, str):
             sc = mapgen.make_config(cfg, seed=mseed, malfunction=mf)
+        elif cfg[0] == "grid":
+            sc = mapgen.generate(cfg[1], cfg[2], cfg[3], seed=mseed, malfunction=mf, name=name)
         elif cfg[0].startswith("flatland"):
             sc = mapgen.from_flatland_params(cfg[1], cfg[1], cfg[2], cfg[3], mseed, malfunction=mf,
                                              max_rails_between_cities=cfg[4], max_rail_pairs_in_city=cfg[5],

@@ -203,3 +203,37 @@ def test_integration_stub_names_the_current_abi():
     doc = open(os.path.join(root, "INTEGRATION.md")).read()
     got = [int(x) for x in re.findall(r"sfl_abi_version\(\) == (\d+)", doc)]
     assert got and all(v == want for v in got), (got, want)
+
+
+def test_link_step_gets_the_extra_flags(tmp_path, monkeypatch):
+    """a tuning build's flags reach hipcc's link line as well as every compile, so link-relevant flags
+    (-fgpu-rdc, sanitizer / profiling / coverage flags, -Wl,...) link the objects they compiled.  (The commands are
+    recorded, not run: a full hipcc build belongs to build().)"""
+    cmds = []
+
+    class P:
+        returncode = 0
+
+        def __init__(self, cmd, **kw):
+            cmds.append(list(cmd))
+            open(cmd[cmd.index("-o") + 1], "wb").close()
+
+        def wait(self):
+            return 0
+
+        def poll(self):
+            return 0
+
+    def run(cmd, **kw):
+        cmds.append(list(cmd))
+        open(cmd[cmd.index("-o") + 1], "wb").close()
+
+    monkeypatch.setattr(build.subprocess, "Popen", P)
+    monkeypatch.setattr(build.subprocess, "run", run)
+    flags = ["-fgpu-rdc", "-Wl,--build-id=sha1"]
+    build.build_hip(out=str(tmp_path / "libx.so"), flags=flags, force=True)
+    compiles = [c for c in cmds if "-c" in c]
+    links = [c for c in cmds if "-shared" in c and "-c" not in c]
+    assert len(compiles) == len(build.TUS) and len(links) == 1
+    for c in compiles + links:
+        assert all(f in c for f in flags), c

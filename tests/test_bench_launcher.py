@@ -50,13 +50,24 @@ def test_gpus_4_host_rehearsal_runs_the_partitioned_leg():
     here on four host-build ranks over gloo end to end: the env-sharded line plus the leg, whose owned Q rows and
     env states are checked against a fused host run (parity ok), with one message exchange and one reply
     exchange per round."""
+    env = _env()
+    env.pop("OMP_NUM_THREADS", None)  # (the ranks bound their host-build threads themselves)
     r = _bench(["--gpus", "4", "--rehearse-on-host", "--config", "c2", "--envs", "4", "--decisions", "32",
-                "--steps", "2", "--warmup", "1", "--verify-envs", "2"], _env(OMP_NUM_THREADS="2"), timeout=600)
+                "--steps", "2", "--warmup", "1", "--verify-envs", "2"], env, timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout
     res = json.loads(lines[0])
     assert res["world_size"] == 4 and res["parity"] == "ok"
+    # the host-build parity check of each rank runs on its share of the granted cores, not one thread per core
+    cores, quota = len(os.sched_getaffinity(0)), None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        quota = None if q == "max" else int(q) / int(per)
+    except OSError:
+        pass
+    granted = max(1, min(cores, int(quota)) if quota else cores)
+    assert res["parity_threads_per_rank"] == max(1, granted // 4), res["parity_reference"]
     leg = res["partition_leg"]
     assert "error" not in leg, leg
     assert leg["world_size"] == 4 and leg["backend"] == "gloo" and leg["parity"] == "ok", leg

@@ -26,14 +26,7 @@ def lib():
     return _lib.load_product()
 
 
-@pytest.fixture(params=["wave", "wave32", "wave8", "scalar"])
-def kernel(request, monkeypatch):
-    """Which device kernel a Batch created inside the test runs (chosen at sfl_create):
-    'wave' = k_wave at the default group size (four envs per wavefront for maps with <= 32 trains: the
-    bench kernel), 'wave32' = two envs per wavefront (what a batch too small to fill the device gets,
-    sfl_engine.h choose_variant), 'wave8' = eight envs per wavefront, one train per lane (the default for
-    maps with <= 8 trains and batches that fill the device; maps with more trains fall back to one env per
-    wavefront), 'scalar' = k_run."""
+def _select_kernel(request, monkeypatch):
     monkeypatch.delenv("SFL_KERNEL", raising=False)
     monkeypatch.delenv("SFL_WAVE_G", raising=False)
     if request.param == "scalar":
@@ -45,6 +38,24 @@ def kernel(request, monkeypatch):
     else:
         monkeypatch.setenv("SFL_WAVE_G", "32")
     return request.param
+
+
+@pytest.fixture(params=["wave", "wave32", "wave8", "scalar"])
+def kernel(request, monkeypatch):
+    """Which device kernel a Batch created inside the test runs (chosen at sfl_create):
+    'wave' = k_wave at the default group size (four envs per wavefront for maps with <= 32 trains: the
+    bench kernel), 'wave32' = two envs per wavefront (what a batch too small to fill the device gets,
+    sfl_engine.h choose_variant), 'wave8' = eight envs per wavefront, one train per lane (the default for
+    maps with <= 8 trains and batches that fill the device; maps with more trains fall back to one env per
+    wavefront), 'scalar' = k_run."""
+    return _select_kernel(request, monkeypatch)
+
+
+@pytest.fixture(params=["wave", "scalar"])
+def part_kernel(request, monkeypatch):
+    """The partitioned local step's kernels: k_wave (one env per wavefront, whatever the fused group size --
+    so the fused kernel's 'wave32' / 'wave8' group sizes are not separate cases here) or k_run."""
+    return _select_kernel(request, monkeypatch)
 
 
 def _check_kernel(b, kernel):
@@ -202,7 +213,7 @@ def test_c5_small_batch(lib, kernel):
 
 @pytest.mark.parametrize("local_rows", [False, True, "block0of4"])
 @pytest.mark.parametrize("cfg,E", [("c2", 256), ("c5", 64), ("golden:city6_s5", 128)])
-def test_partitioned_rounds_gpu_equal_fused(lib, cfg, E, kernel, local_rows):
+def test_partitioned_rounds_gpu_equal_fused(lib, cfg, E, part_kernel, local_rows):
     """Graph-partitioned mode (BASELINE configs[4]) on the GPU, one rank: the owner-side Q rows,
     the request / reply / update round trips through device buffers, bit-equal to the fused kernel.
     kernel: the local step on k_wave (observe / apply passes, PART) or on the lane-per-env body;
@@ -210,8 +221,7 @@ def test_partitioned_rounds_gpu_equal_fused(lib, cfg, E, kernel, local_rows):
     row operation as a message (decisions + 1 rounds), or keeps only block 0 of a 4-rank partition
     in place (a 4-rank job's message traffic on one rank)."""
     import torch
-    if kernel in ("wave32", "wave8"):
-        pytest.skip("the partitioned local step runs one env per wavefront whatever the fused group size")
+    kernel = part_kernel
     part = importlib.import_module("network-distributed-q-learning_amd.partition")
     sc = _golden.load(cfg[7:])["scenario_obj"] if cfg.startswith("golden:") else mapgen.make_config(cfg)
     cm = comp.compile_scenario(sc)
@@ -597,9 +607,14 @@ def test_aec_replay_golden_gpu(lib, name):
     (observation, reward, mask, successor, arrivals, time, semaphore-table digest)."""
     from tests import aec_replay
     g = _golden.load(name)
-    n = aec_replay.replay(g, g["learn"]["events"], lib)
-    assert n == sum(1 for e in g["learn"]["events"] if e[0] == "D")
-    aec_replay.replay(g, g["test"]["events"], lib)
+    n_dec = sum(1 for e in g["learn"]["events"] if e[0] == "D")
+    # (each step is a launch plus host reads of the env's state; the > 4,000-decision runs -- c5_mf's 256 switches /
+    # 128 trains, grid100x48_s3 -- replay a 3,000-decision prefix of learn() and of test() with the semaphore digest
+    # every 4th step; the host build replays every event of them, tests/test_aec.py)
+    cap, every = (3000, 4) if n_dec > 4000 else (None, 1)
+    n = aec_replay.replay(g, g["learn"]["events"], lib, digest_every=every, max_decisions=cap)
+    assert n == (n_dec if cap is None else min(cap, n_dec))
+    aec_replay.replay(g, g["test"]["events"], lib, digest_every=every, max_decisions=cap)
 
 
 @pytest.mark.parametrize("cfg", ["c2", "c3"])

@@ -229,6 +229,41 @@ def test_multi_rank_cohorts_match_fused(world, k_init):
     two_rank_run("c5", world=world, cohorts=2, k_init=k_init)
 
 
+def _short_rank_worker(rank, world, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world), RANK=str(rank),
+                          LOCAL_RANK=str(rank))
+        par = importlib.import_module("network-distributed-q-learning_amd.parallel")
+        dist = par.init("gloo")
+        cm = comp.compile_scenario(mapgen.make_config("c2"))
+        n = [3, 1][rank]  # rank 1 has one env: too few for two cohorts
+        try:
+            part.CohortPipeline(cm, HP, list(range(n)), [0, 3][rank], 4, cohorts=2, rank=rank, world=world, dist=dist,
+                                lib=hostsim.lib(), ntab=4096, buffer_device="cpu")
+            q.put((rank, "no error"))
+        except ValueError as ex:
+            q.put((rank, "ValueError" if "cannot each form 2 cohorts" in str(ex) else repr(ex)))
+        dist.destroy_process_group()
+    except Exception as ex:
+        q.put((rank, repr(ex)))
+        raise
+
+
+def test_cohort_shortage_on_one_rank_raises_on_every_rank():
+    """a rank with fewer envs than cohorts must not raise alone while its peers wait in the collective
+    env-count all-reduce: every rank raises, and none hangs."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_short_rank_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=300) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+    assert res == [(0, "ValueError"), (1, "ValueError")], res
+
+
 def test_two_rank_1024_decision_step_syncs_only_at_checkpoints():
     """Two gloo ranks, one 1,024-decision step: the rounds between checkpoints run without the host
     reading a count (fixed-size segments; the ranks agree on their size at the checkpoints), the
