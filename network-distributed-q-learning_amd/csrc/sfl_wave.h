@@ -110,6 +110,14 @@ __device__ __forceinline__ int32_t d16_lo(uint32_t w) {
   return v == -32768 ? (int32_t)0x80000000 : (v == 32767 ? DIST_INF : v);
 }
 __device__ __forceinline__ int32_t d16_hi(uint32_t w) { return d16_lo(w >> 16); }
+// epsilon staged with the batch (round 6): the grouped shapes (G < 64, <= 64 switches) stage, with each queued
+// train's record, eps_tab[n] of its decision switch as the switch's interaction count n stands at staging (record
+// double 3); the decision compares against it instead of loading eps_tab[n] behind the count (one dependent vector
+// load off the decision's chain).  A switch decided on since the staging has a stale value (its count moved): the
+// env's LDS word lrng[5] marks those switches, and their decisions load eps_tab[n] as before.  0: off (A/B builds)
+#ifndef SFL_EPS_PF
+#define SFL_EPS_PF 1
+#endif
 #ifndef SFL_WAVE_BLOCK
 #define SFL_WAVE_BLOCK 256  // threads per k_wave block (envs per block x 64)
 #endif
@@ -332,6 +340,10 @@ struct WEnv {
   static constexpr int RING_N = G < 64 ? SFL_PF_RING : SFL_PF_RING64;
   static constexpr bool RING = !PART && TPL > 1 && RING_N > 0 && RING_N < TWc;
   static constexpr int PF_SLOTS = PART ? 1 : (RING ? RING_N : TWc);
+  // (SFL_EPS_PF) the record's doubles: + the staged epsilon
+  static constexpr bool EPS_PF = SFL_EPS_PF && !PART && G < 64 && G * SPL <= 64;
+  static constexpr int PFD = EPS_PF ? PF_D + 1 : PF_D;
+  static constexpr int PFW = 2 * PFD + PF_WI;
   __device__ __forceinline__ static int pfx(int h) { return PART ? 0 : h; }
   // RING: record i is staged by lane i % G (register slot i / G) in one pass per G records -- the lanes
   // stage the batch's queued trains in queue order, so a batch of up to G decisions is one set of
@@ -365,7 +377,7 @@ struct WEnv {
   uint32_t* lcnt;  // [64*SPL]
   // batch prefetch (see prefetch()): per queued train (lane), the staged Q row, the pending
   // update's Q cell value and the slot word in LDS, and the staged offsets in VGPRs
-  double* lpf;       // [TW][PF_D]: pending cell value | slot word (as bits) | row max
+  double* lpf;       // [TW][PFD]: pending cell value | slot word (as bits) | row max (| staged epsilon)
   uint32_t* lpi;     // [TW][PF_WI]: int16 distances, argmaxes
   uint32_t pf_roff[PFS];  // offset of the staged row in the env's Q block (PF_NONE: none)
   uint32_t pf_qoff[PFS];  // offset of the staged pending cell (PF_NONE: none)
@@ -382,7 +394,7 @@ struct WEnv {
   Mask q_mask, arr_mask, fl_mask, mf_mask;
   // the epsilon-greedy stream (numpy PCG64 state, increment, buffered half) lives in LDS: it is
   // touched once per decision and would otherwise hold ten registers across the whole loop
-  uint64_t* lrng;  // [6]: state hi, lo, inc hi, lo, has << 32 | buf
+  uint64_t* lrng;  // [6]: state hi, lo, inc hi, lo, has << 32 | buf, (EPS_PF) switches decided since the staging
   int64_t cum;     // cumulative reward: a sum of integer rewards, exact in f64 (converted on store)
   int32_t n_mf, ep_dec, ep_ticks;
   int32_t step_ctr;
@@ -430,12 +442,12 @@ struct WEnv {
     for (int k = 0; k < TPL; ++k) mine[k] = lane + G * k < m_.T;
 #pragma unroll
     for (int k = 0; k < PFS; ++k) pf_roff[k] = pf_qoff[k] = PF_NONE;
-    lpi = (uint32_t*)(lpf + PF_SLOTS * PF_D);
-    lrng = (uint64_t*)(lds + G * (PPL + SPL) + PF_SLOTS * PF_WORDS);
+    lpi = (uint32_t*)(lpf + PF_SLOTS * PFD);
+    lrng = (uint64_t*)(lds + G * (PPL + SPL) + PF_SLOTS * PFW);
     // PART: the timetable rows are read from the map (L2-resident): a launch runs one or two
     // decisions, so a per-launch LDS copy would cost more than it saves
     if constexpr (PART) ltt = m.tr_pack;
-    else ltt = ltt_shared ? ltt_shared : (const int32_t*)(lds + G * (PPL + SPL) + PF_SLOTS * PF_WORDS + 12);
+    else ltt = ltt_shared ? ltt_shared : (const int32_t*)(lds + G * (PPL + SPL) + PF_SLOTS * PFW + 12);
     pf_ok = false;
     if constexpr (PART) {  // the rows this rank owns, of this env (the env-local table is freed)
       const size_t ge = (size_t)P_->env_base + e_;
@@ -1486,6 +1498,7 @@ struct WEnv {
 #pragma unroll
     for (int k = 0; k < PFS; ++k) pf_roff[k] = pf_qoff[k] = PF_NONE;
     pf_n = 0;
+    if constexpr (EPS_PF) lrng[5] = 0ull;  // (uniform value from every lane) the staged epsilons are current
     if constexpr (PF_BY_RANK) {
       // lane i stages the i-th queued train (record i = the i-th decision of the batch); trains beyond the
       // records wait for the next staging
@@ -1549,7 +1562,7 @@ struct WEnv {
     const int slot = pin & 3;
     const int dir0 = (int)tb_dir(bits_k);
     const int pos0 = pos_k >= 0 ? pos_k : 0;
-    double* pfl = lpf + PF_D * rec;
+    double* pfl = lpf + PFD * rec;
     uint32_t* pfi = lpi + PF_WI * rec;
     // level 1: slot word, switch record, timetable row, the row block's port record, first moves
     const uint64_t slw = ld(sbase(), slot_ix(sw, hk));
@@ -1562,6 +1575,13 @@ struct WEnv {
     const uint32_t a1 = n_plan ? pl_front(plan_k) : A_FWD;
     // move-table rows (all four rail actions) at the cell and after the first rail action
     const u4 row0 = ld((const u4*)m.move_tab, (size_t)((uint32_t)pos0 * 4u + (uint32_t)dir0));
+    // (EPS_PF) eps0 * decay**n of the decision switch at its present count (distr_q.py:59-68); beyond the table the
+    // decision computes it
+    double eps_v = 0.0;
+    if constexpr (EPS_PF) {
+      const uint32_t n_s = cget_var(sw);
+      if (!greedy && n_s < (uint32_t)m.ntab) eps_v = ld(m.eps_tab, (size_t)n_s);
+    }
     auto mv_in = [](const u4& r, uint32_t a) -> Move {
       const uint32_t q = a & 3u;
       return unpack_move(q == 0 ? r[0] : q == 1 ? r[1] : q == 2 ? r[2] : r[3]);
@@ -1678,6 +1698,7 @@ struct WEnv {
     }
     pfl[0] = qv;
     pfl[1] = __longlong_as_double((long long)slw);
+    if constexpr (EPS_PF) pfl[3] = eps_v;
     pfi[0] = d16(dd) | (d16(d_stop) << 16);
     pfi[1] = d16(d_rt[1]) | (d16(d_rt[2]) << 16);
     roff_out = (row_ok && !PART) ? roff : PF_NONE;
@@ -1742,7 +1763,7 @@ struct WEnv {
     const vec_t<int32_t, 8> tr = tr_row(h);
     const int rec = RING ? pf_n : pfx(h);
     if constexpr (RING) pf_n += 1;
-    const double* pfh = lpf + PF_D * rec;
+    const double* pfh = lpf + PFD * rec;
     const uint32_t* pfw = lpi + PF_WI * rec;
     // the decision's LDS reads that do not depend on its observation, issued together: the staged
     // slot word (never stale: a decision writes only its own train's slots), row column, pending
@@ -1756,6 +1777,8 @@ struct WEnv {
 #pragma unroll
     for (int i = 0; i < 5; ++i) rng_w[i] = lrng[i];
     const uint32_t n_sw = cget(sw);
+    const double pf_eps = EPS_PF ? pfh[EPS_PF ? 3 : 0] : 0.0;     // the staged epsilon of this switch
+    const uint64_t dec_sw = EPS_PF ? U(lrng[EPS_PF ? 5 : 0]) : 0ull;  // switches decided since the staging
     const int pidx = PF_BY_RANK ? rec : h;  // the staged offsets' record
     const uint32_t pf_roff_h = rec_of(pf_roff, pidx), pf_qoff_h = rec_of(pf_qoff, pidx);
     const int np = swr.np();
@@ -1862,6 +1885,8 @@ struct WEnv {
       const double ud = Ud(pcg_double(rng));
       if (xp::kEpsConst) {
         explore = ud < m.eps0;
+      } else if (EPS_PF && !((dec_sw >> sw) & 1ull) && n < (uint32_t)m.ntab) {
+        explore = ud < Ud(pf_eps);  // staged with the batch at this same count n
       } else {
         explore = ud < (n < (uint32_t)m.ntab ? LDC(m.eps_tab, (size_t)n) : m.eps0 * pow_ool(m.eps_decay, (double)n));
       }
@@ -1898,6 +1923,7 @@ struct WEnv {
         lrng[4] = ((uint64_t)rng.has << 32) | rng.buf;
       }
     }
+    if constexpr (EPS_PF) lrng[5] = dec_sw | (1ull << sw);  // (uniform) this switch's count moves in post
     if constexpr (PART) {
       if (observe_only) {
         emit_req(sw, slot, state, amask, explore);
@@ -2351,7 +2377,7 @@ __device__ void run(const SflMap& m, const SflState& s, const SflCtl& c, const S
   // semaphores, counters, prefetch records, rng, timetable (PART: one record, timetable from the map)
   // (PART: the launch's initial records / counters in place of the timetable copy)
   constexpr int LDS_WORDS =
-      64 * (PPL + SPL) + V::PF_SLOTS * PF_WORDS + 12 + (PART ? 64 * PPL + 2 * SPL + 6 * 64 * V::TPL : TW * 8);
+      64 * (PPL + SPL) + V::PF_SLOTS * V::PFW + 12 + (PART ? 64 * PPL + 2 * SPL + 6 * 64 * V::TPL : TW * 8);
   const int lane = (int)__lane_id();
   const uint32_t e = uni((uint32_t)((blockIdx.x * blockDim.x + threadIdx.x) >> 6));
   if (e >= s.E) return;
@@ -2359,7 +2385,7 @@ __device__ void run(const SflMap& m, const SflState& s, const SflCtl& c, const S
   __shared__ uint32_t lds[WPB * LDS_WORDS];
   V v(m, s, e, lane, lds + (threadIdx.x >> 6) * LDS_WORDS, P);
   if constexpr (PART) {
-    v.lsem0 = lds + (threadIdx.x >> 6) * LDS_WORDS + 64 * (PPL + SPL) + V::PF_SLOTS * PF_WORDS + 12;
+    v.lsem0 = lds + (threadIdx.x >> 6) * LDS_WORDS + 64 * (PPL + SPL) + V::PF_SLOTS * V::PFW + 12;
     v.ldirty = v.lsem0 + 64 * PPL;
     v.ltr0 = v.ldirty + 2 * SPL;
   }
@@ -2551,7 +2577,7 @@ __device__ void run_groups(const SflMap& m, const SflState& s, const SflCtl& c) 
   // per env: semaphores, counters, prefetch records, rng; per block: the timetable rows and the
   // per-switch / per-port map records (the groups of a wave read different switches' records: LDS
   // reads instead of vector loads)
-  constexpr int LDS_WORDS = (G * (PPL + SPL) + V::PF_SLOTS * PF_WORDS + 12 + 3) / 4 * 4;
+  constexpr int LDS_WORDS = (G * (PPL + SPL) + V::PF_SLOTS * V::PFW + 12 + 3) / 4 * 4;
   constexpr int EPB = SFL_GROUP_BLOCK / G;  // envs per block (sfl.hip launches)
   constexpr int SWX = G * SPL, NPX = G * PPL;  // switches / ports the shape holds
   constexpr int O_TT = EPB * LDS_WORDS, O_SW = O_TT + TW * 8, O_PP = O_SW + SWX * V::SW_LDS, O_PT = O_PP + NPX * 4;

@@ -17,7 +17,8 @@
 #   c5fused    c5 fused at 16,384 envs
 #   part       the 8-rank partition rehearsal on one GPU (with the env-sharded fused comparison)
 #   ab         bench for each library in LIBS (SFL_LIB, --experimental for all but libsfl)
-#   eval       the published evaluation table (scripts/eval_table.py) through libsfl.so
+#   eval       the published evaluation table (scripts/eval_table.py) through libsfl.so, 15 trains
+#   eval100    one 100-train learning run + greedy evaluation through libsfl.so (SEEDS100, default 66)
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
@@ -79,16 +80,21 @@ for S in "$@"; do
       line $OUT/part.json
       python -c "import json;d=json.load(open('$OUT/part.json'));print('  fused env-sharded %.1fM/s, vs_env_sharded_fused %.3f' % (d['env_sharded_fused']['value']/1e6, d['vs_env_sharded_fused']))" ;;
     ab)
+      i=0
       for L in ${LIBS:-libsfl}; do
+        i=$((i+1))
         export SFL_LIB=$GRAFT_REPO_ROOT/network-distributed-q-learning_amd/$L.so
         V="--verify-envs ${VERIFY_ENVS:-0} --experimental"; [ "$L" = "libsfl" ] && V=""
-        timeout -k 10 300 python bench.py --steps ${STEPS:-10} --warmup 2 --no-cpu $V ${BENCH_ARGS} > $OUT/ab_${L}.json 2> $OUT/ab_${L}.err; ok $? "ab $L"
-        line $OUT/ab_${L}.json
+        timeout -k 10 300 python bench.py --steps ${STEPS:-10} --warmup 2 --no-cpu --sustain-seconds 0 $V ${BENCH_ARGS} > $OUT/ab_${i}_${L}.json 2> $OUT/ab_${i}_${L}.err; ok $? "ab $L"
+        line $OUT/ab_${i}_${L}.json
       done
       unset SFL_LIB ;;
-    eval)
-      timeout -k 10 900 python -u scripts/eval_table.py $OUT/eval_table.json ${EVAL_ARGS} > $OUT/eval_table.log 2>&1; rc=$?
-      tail -20 $OUT/eval_table.log; ok $rc "eval" ;;
+    eval)  # the 15-train sweep config with malfunctions, 3 seeds x 10 evaluations, vs the host build's run
+      timeout -k 10 900 python -u scripts/eval_table.py $OUT/eval_table.json --compare profiles/r06_eval_table_host.json ${EVAL_ARGS} > $OUT/eval_table.log 2>&1; rc=$?
+      grep -v "^\.\.\." $OUT/eval_table.log | tail -6; ok $rc "eval" ;;
+    eval100)  # one 100-train learning run (the two-slot k_wave shape) vs the host build's run of the same seed
+      timeout -k 10 1000 python -u scripts/eval_table.py $OUT/eval100.json --trains 100 --size 100 --cities 25 --mf 0,0,0 --seeds ${SEEDS100:-66} --compare profiles/r06_100_trains_host.json > $OUT/eval100.log 2>&1; rc=$?
+      grep -v "^\.\.\." $OUT/eval100.log | tail -6; ok $rc "eval100" ;;
     *)
       echo "unknown step $S"; exit 2 ;;
   esac
