@@ -114,9 +114,13 @@ __device__ __forceinline__ int32_t d16_hi(uint32_t w) { return d16_lo(w >> 16); 
 // train's record, eps_tab[n] of its decision switch as the switch's interaction count n stands at staging (record
 // double 3); the decision compares against it instead of loading eps_tab[n] behind the count (one dependent vector
 // load off the decision's chain).  A switch decided on since the staging has a stale value (its count moved): the
-// env's LDS word lrng[5] marks those switches, and their decisions load eps_tab[n] as before.  0: off (A/B builds)
+// env's LDS word lrng[5] marks those switches, and their decisions load eps_tab[n] as before.  Measured and NOT the
+// default (profiles/r06e_eps_staging_ab.txt, same box, parity ok): c3 1,590-1,593 M vs 1,611-1,612 M, c2 at 4,096
+// envs 335.5 M vs 345.6 M -- the staged value's live range and the lrng[5] read-modify-write cost the variant-7 kernel
+// 12 more spill instructions (40 -> 52, scripts/spills.py), some of them in the decision and staging paths, and the
+// staging adds a counter read and a load to every staged record.  1: on (A/B builds)
 #ifndef SFL_EPS_PF
-#define SFL_EPS_PF 1
+#define SFL_EPS_PF 0
 #endif
 #ifndef SFL_WAVE_BLOCK
 #define SFL_WAVE_BLOCK 256  // threads per k_wave block (envs per block x 64)
@@ -1575,13 +1579,6 @@ struct WEnv {
     const uint32_t a1 = n_plan ? pl_front(plan_k) : A_FWD;
     // move-table rows (all four rail actions) at the cell and after the first rail action
     const u4 row0 = ld((const u4*)m.move_tab, (size_t)((uint32_t)pos0 * 4u + (uint32_t)dir0));
-    // (EPS_PF) eps0 * decay**n of the decision switch at its present count (distr_q.py:59-68); beyond the table the
-    // decision computes it
-    double eps_v = 0.0;
-    if constexpr (EPS_PF) {
-      const uint32_t n_s = cget_var(sw);
-      if (!greedy && n_s < (uint32_t)m.ntab) eps_v = ld(m.eps_tab, (size_t)n_s);
-    }
     auto mv_in = [](const u4& r, uint32_t a) -> Move {
       const uint32_t q = a & 3u;
       return unpack_move(q == 0 ? r[0] : q == 1 ? r[1] : q == 2 ? r[2] : r[3]);
@@ -1663,6 +1660,14 @@ struct WEnv {
       for (int c = 0; c < 4; ++c) rv[c] = ld(rp, (size_t)((uint32_t)c < w ? c : 0));
       qv = ld(qbase(), (size_t)(hp ? qoff : 0u));
     }
+    // (EPS_PF) eps0 * decay**n of the decision switch at its present count (distr_q.py:59-68), with the Q loads (a
+    // short live range); beyond the table the decision computes it
+    if constexpr (EPS_PF) {
+      const uint32_t n_s = cget_var(sw);
+      double eps_v = 0.0;
+      if (!greedy && n_s < (uint32_t)m.ntab) eps_v = ld(m.eps_tab, (size_t)n_s);
+      pfl[3] = eps_v;
+    }
     // the greedy choice on the staged row (distr_q.py:449-490, as in decide): valid whenever the
     // row is (a decision uses it only if its observation is the staged one)
     {
@@ -1698,7 +1703,6 @@ struct WEnv {
     }
     pfl[0] = qv;
     pfl[1] = __longlong_as_double((long long)slw);
-    if constexpr (EPS_PF) pfl[3] = eps_v;
     pfi[0] = d16(dd) | (d16(d_stop) << 16);
     pfi[1] = d16(d_rt[1]) | (d16(d_rt[2]) << 16);
     roff_out = (row_ok && !PART) ? roff : PF_NONE;
@@ -1777,8 +1781,6 @@ struct WEnv {
 #pragma unroll
     for (int i = 0; i < 5; ++i) rng_w[i] = lrng[i];
     const uint32_t n_sw = cget(sw);
-    const double pf_eps = EPS_PF ? pfh[EPS_PF ? 3 : 0] : 0.0;     // the staged epsilon of this switch
-    const uint64_t dec_sw = EPS_PF ? U(lrng[EPS_PF ? 5 : 0]) : 0ull;  // switches decided since the staging
     const int pidx = PF_BY_RANK ? rec : h;  // the staged offsets' record
     const uint32_t pf_roff_h = rec_of(pf_roff, pidx), pf_qoff_h = rec_of(pf_qoff, pidx);
     const int np = swr.np();
@@ -1885,10 +1887,16 @@ struct WEnv {
       const double ud = Ud(pcg_double(rng));
       if (xp::kEpsConst) {
         explore = ud < m.eps0;
-      } else if (EPS_PF && !((dec_sw >> sw) & 1ull) && n < (uint32_t)m.ntab) {
-        explore = ud < Ud(pf_eps);  // staged with the batch at this same count n
       } else {
-        explore = ud < (n < (uint32_t)m.ntab ? LDC(m.eps_tab, (size_t)n) : m.eps0 * pow_ool(m.eps_decay, (double)n));
+        // (EPS_PF) the staged value, unless the switch was decided on since the staging (its count moved)
+        bool staged = false;
+        double eps_st = 0.0;
+        if constexpr (EPS_PF) {
+          staged = !((lrng[5] >> sw) & 1ull) && n < (uint32_t)m.ntab;
+          eps_st = pfh[3];
+        }
+        explore = ud < (staged ? eps_st
+                               : (n < (uint32_t)m.ntab ? LDC(m.eps_tab, (size_t)n) : m.eps0 * pow_ool(m.eps_decay, (double)n)));
       }
       if (explore && !observe_only) {
         const uint32_t sub_seed = pcg_bounded(rng, 2147483646u);
@@ -1923,7 +1931,7 @@ struct WEnv {
         lrng[4] = ((uint64_t)rng.has << 32) | rng.buf;
       }
     }
-    if constexpr (EPS_PF) lrng[5] = dec_sw | (1ull << sw);  // (uniform) this switch's count moves in post
+    if constexpr (EPS_PF) lrng[5] |= 1ull << sw;  // (uniform) this switch's count moves in post
     if constexpr (PART) {
       if (observe_only) {
         emit_req(sw, slot, state, amask, explore);
