@@ -52,6 +52,9 @@ PUBLISHED = {15: dict(early=10.9, late=1.6, not_arrived=2.5, what="plot.ipynb ce
                                                                      "5 seeds x 1 evaluation")}
 
 
+HP_SWEEP = dict(gamma=1.0, epsilon=0.5, epsilon_decay_rate=0.9997, lr=0.1, lr_decay_rate=1.0, default_q=0.0)
+
+
 def classify(delays, trains_at_dest, n_trains):
     """plot.ipynb cell 15, literally: (early, late, not_arrived), or None when cell 15 would fail (fewer delays than
     trains: its mask & delays cannot broadcast)."""
@@ -112,6 +115,15 @@ def main():
     import eval as entry_eval
 
     work = args.work or tempfile.mkdtemp(prefix="sfl_eval_")
+    # a progress line every 30 s (a learn() call of many episodes prints nothing until its first checkpoint)
+    import threading
+    t_start = time.time()
+
+    def heartbeat():
+        while True:
+            time.sleep(30)
+            print(f"... {time.time() - t_start:.0f} s", flush=True)
+    threading.Thread(target=heartbeat, daemon=True).start()
     res = {"config": f"hyperparam_tuning.py:17-35 keys: {args.size} x {args.size}, max_num_cities {args.cities}, "
                      f"max_rails_between_cities 2, max_rail_pairs_in_city 2, {args.trains} trains, malfunctions "
                      f"{args.mf}, {args.episodes} episodes, checkpoint {args.checkpoint_freq}, exploit {args.exploit_freq}",
@@ -144,11 +156,22 @@ def main():
                 rows.append(row)
         arrived_learn = np.load(os.path.join(exp_dir, "arrived_trains.npz"))["x"]
         qd, nkeys = q_digest(os.path.join(exp_dir, "distr_q_model.pkl"))
+        kern = None
+        if not args.host:  # the device kernel this map runs on (k_wave variant, lanes per env)
+            import configparser as _cp
+            runtime = importlib.import_module("network-distributed-q-learning_amd.runtime")
+            comp = importlib.import_module("network-distributed-q-learning_amd.compiler")
+            c = _cp.ConfigParser()
+            c.read(cfg)
+            kb = runtime.Batch(comp.compile_scenario(entry_main.build_scenario(c)), HP_SWEEP, [seed])
+            cn = kb.counters()
+            kern = {"kernel_variant": cn["kernel_variant"], "group_lanes": cn["group_lanes"]}
+            kb.close()
         cr, arr, dl = runs[0]
         res["seeds"][str(seed)] = dict(
             evals=n_ev, table_per_eval=per, eval_cum_reward=[float(r[0]) for r in runs],
             eval_arrived=[int(r[1]) for r in runs], eval_delays_first=[float(x) for x in dl],
-            learn_mean_arrived_last_500=float(np.mean(arrived_learn[-500:])), q_sha1=qd, q_keys=nkeys,
+            learn_mean_arrived_last_500=float(np.mean(arrived_learn[-500:])), q_sha1=qd, q_keys=nkeys, kernel=kern,
             learn_seconds=t_learn, seconds=time.time() - t0)
         print(f"seed {seed}: learn {t_learn:.1f} s, last-500 mean arrived {np.mean(arrived_learn[-500:]):.2f} / "
               f"{args.trains}; eval {per[0]} x {n_ev}, Q {qd[:12]} ({nkeys} keys)", flush=True)

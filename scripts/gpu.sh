@@ -13,6 +13,7 @@
 #   waitsplit  the wave-time split per decision (scripts/pmc_per_dec.py; DEC = decisions per launch)
 #   c2         configs[1] (c2 at its 4,096 envs): ktrace + traffic passes + waitsplit, THEN its bench line (so the
 #              line carries the counter profile of its own build: commit profiles/<tag>_c2_4096_pmc.json first)
+#   c2dec      configs[1] at 1,024 / 4,096 / 16,384 decisions per env and launch (C2DEC)
 #   c2big      c2 at 65,536 envs
 #   c5fused    c5 fused at 16,384 envs
 #   part       the 8-rank partition rehearsal on one GPU (with the env-sharded fused comparison)
@@ -68,6 +69,11 @@ for S in "$@"; do
       TAG=${TAG:-gpu}/c2 BENCH_ARGS="$B --verify-envs 0" DEC=$((4096*1024)) bash scripts/gpu_waitsplit.sh; ok $? "c2 waitsplit"
       timeout -k 10 300 python bench.py $B --steps 10 --warmup 2 --no-cpu > $OUT/c2_bench.json 2> $OUT/c2_bench.err; ok $? "c2 bench"
       line $OUT/c2_bench.json ;;
+    c2dec)  # configs[1] at longer launches (decisions per env per step): does the one-generation tail amortise?
+      for D in ${C2DEC:-1024 4096 16384}; do
+        timeout -k 10 300 python bench.py --config c2 --envs 4096 --decisions $D --steps $((10240 / D > 2 ? 10240 / D : 2)) --warmup 1 $SHORT > $OUT/c2_dec$D.json 2> $OUT/c2_dec$D.err; ok $? "c2 decisions $D"
+        line $OUT/c2_dec$D.json
+      done ;;
     c2big)
       timeout -k 10 300 python bench.py --config c2 --steps 10 --warmup 2 --no-cpu > $OUT/c2_65536_bench.json 2> $OUT/c2_65536.err; ok $? "c2 65536"
       line $OUT/c2_65536_bench.json ;;
