@@ -11,8 +11,9 @@
 #   ktrace     rocprofv3 --kernel-trace --stats of a short bench (BENCH_ARGS)
 #   pmc        the HBM-traffic passes (FETCH_SIZE, WRITE_SIZE, L2 hit/miss, memory-side requests) of a short bench
 #   waitsplit  the wave-time split per decision (scripts/pmc_per_dec.py; DEC = decisions per launch)
-#   c2         configs[1] (c2 at its 4,096 envs): ktrace + traffic passes + waitsplit, THEN its bench line (so the
-#              line carries the counter profile of its own build: commit profiles/<tag>_c2_4096_pmc.json first)
+#   final      the committed build's evidence: ktrace + traffic passes + waitsplit, summarised into
+#              profiles/$PTAG_pmc.json on the box, THEN the default and the driver-style bench lines (which attach it)
+#   c2         the same for configs[1] (c2 at its 4,096 envs): profiles/$PTAG_c2_4096_pmc.json, then its bench line
 #   c2dec      configs[1] at 1,024 / 4,096 / 16,384 decisions per env and launch (C2DEC)
 #   c2big      c2 at 65,536 envs
 #   c5fused    c5 fused at 16,384 envs
@@ -62,11 +63,26 @@ for S in "$@"; do
       pmc $OUT ${BENCH_ARGS} ;;
     waitsplit)
       TAG=${TAG:-gpu} bash scripts/gpu_waitsplit.sh; ok $? "waitsplit" ;;
+    final)  # the committed build's evidence: kernel stats, traffic passes, wave-time split, their summary as
+            # profiles/${PTAG}_pmc.json (bench.py attaches it by build id), then the default and the driver's bench lines
+      P=${PTAG:-${TAG:-gpu}}
+      ktrace $OUT/prof; ok $? "ktrace"
+      pmc $OUT
+      TAG=${TAG:-gpu} bash scripts/gpu_waitsplit.sh > $OUT/waitsplit.log; ok $? "waitsplit"
+      python scripts/pmc_summary.py $OUT profiles/${P}_pmc.json $OUT/prof.json > $OUT/pmc_summary.log; ok $? "pmc summary"
+      cp profiles/${P}_pmc.json $OUT/
+      timeout -k 10 600 python bench.py > $OUT/bench.json 2> $OUT/bench.err; rc=$?
+      [ $rc -eq 0 ] || tail -5 $OUT/bench.err; ok $rc "bench"; line $OUT/bench.json
+      timeout -k 10 600 python bench.py --steps 20 --warmup 5 > $OUT/driver.json 2> $OUT/driver.err; rc=$?
+      [ $rc -eq 0 ] || tail -5 $OUT/driver.err; ok $rc "driver"; line $OUT/driver.json ;;
     c2)
+      P=${PTAG:-${TAG:-gpu}}
       B="--config c2 --envs 4096"
       ktrace $OUT/c2_prof $B; ok $? "c2 ktrace"
       pmc $OUT/c2 $B
-      TAG=${TAG:-gpu}/c2 BENCH_ARGS="$B --verify-envs 0" DEC=$((4096*1024)) bash scripts/gpu_waitsplit.sh; ok $? "c2 waitsplit"
+      TAG=${TAG:-gpu}/c2 BENCH_ARGS="$B --verify-envs 0" DEC=$((4096*1024)) bash scripts/gpu_waitsplit.sh > $OUT/c2_waitsplit.log; ok $? "c2 waitsplit"
+      python scripts/pmc_summary.py $OUT/c2 profiles/${P}_c2_4096_pmc.json $OUT/c2_prof.json > $OUT/c2_pmc_summary.log; ok $? "c2 pmc summary"
+      cp profiles/${P}_c2_4096_pmc.json $OUT/
       timeout -k 10 300 python bench.py $B --steps 10 --warmup 2 --no-cpu > $OUT/c2_bench.json 2> $OUT/c2_bench.err; ok $? "c2 bench"
       line $OUT/c2_bench.json ;;
     c2dec)  # configs[1] at longer launches (decisions per env per step): does the one-generation tail amortise?
