@@ -659,12 +659,12 @@ struct HipBackend {
   {                                                                                                             \
     constexpr sfl::WaveShape w = sfl::kVariants[v];                                                             \
     const unsigned gblocks = (unsigned)(((size_t)s.E * w.G + SFL_GROUP_BLOCK - 1) / SFL_GROUP_BLOCK);             \
-    if (c.trace) k_wave_g<w.PPL, w.SPL, w.TW, true, w.G, w.OCC><<<gblocks, SFL_GROUP_BLOCK, 0, stream>>>(pm, ps, pc); \
+    if (c.trace) k_wave_g<w.PPL, w.SPL, w.TW, true, w.G, w.OCC, false, (bool)w.LM><<<gblocks, SFL_GROUP_BLOCK, 0, stream>>>(pm, ps, pc); \
     else if (c.phase_cyc)                                                                                       \
-      k_wave_g<w.PPL, w.SPL, w.TW, false, w.G, w.OCC, true><<<gblocks, SFL_GROUP_BLOCK, 0, stream>>>(pm, ps, pc); \
-    else k_wave_g<w.PPL, w.SPL, w.TW, false, w.G, w.OCC><<<gblocks, SFL_GROUP_BLOCK, 0, stream>>>(pm, ps, pc);   \
+      k_wave_g<w.PPL, w.SPL, w.TW, false, w.G, w.OCC, true, (bool)w.LM><<<gblocks, SFL_GROUP_BLOCK, 0, stream>>>(pm, ps, pc); \
+    else k_wave_g<w.PPL, w.SPL, w.TW, false, w.G, w.OCC, false, (bool)w.LM><<<gblocks, SFL_GROUP_BLOCK, 0, stream>>>(pm, ps, pc); \
   }
-    static_assert(sfl::kVariants[5].TW > 64 && sfl::kNumVariants == 11, "variant 5 is the two-slot shape, 6-10 grouped");
+    static_assert(sfl::kVariants[5].TW > 64 && sfl::kNumVariants == 12, "variant 5 is the two-slot shape, 6-11 grouped");
     if (variant == 1) SFL_KW(1)
     else if (variant == 2) SFL_KW(2)
     else if (variant == 3) SFL_KW(3)
@@ -675,6 +675,7 @@ struct HipBackend {
     else if (variant == 8) SFL_KG(8)
     else if (variant == 9) SFL_KG(9)
     else if (variant == 10) SFL_KG(10)
+    else if (variant == 11) SFL_KG(11)
 #undef SFL_KG
 #undef SFL_KW2
 #undef SFL_KW

@@ -112,14 +112,30 @@ struct Handle {
 #endif
 struct WaveShape {
   int PPL, SPL, TW, G, OCC;
+  int LM = 0;  // 1: the map's move table and distance map are copied into the block's LDS (run_groups, round 6)
 };
+#ifndef SFL_LM_OCC
+#define SFL_LM_OCC 4  // variant 11's register budget (waves per SIMD)
+#endif
 #ifndef SFL_V7_OCC
 #define SFL_V7_OCC 4  // variant 7 (c3): waves per SIMD its registers are budgeted for (tuning builds: 3)
 #endif
 constexpr WaveShape kVariants[] = {{0, 0, 0, 64, 0},    {1, 1, 32, 64, 0},  {4, 1, 32, 64, 0}, {4, 1, 64, 64, 0},
                                    {8, 2, 64, 64, 0},   {16, 4, 128, 64, 0}, {4, 1, 16, 16, 4}, {16, 4, 32, 16, SFL_V7_OCC},
-                                   {2, 1, 32, 32, 4},   {8, 2, 32, 32, 4},   {8, 2, 8, 8, SFL_G8_OCC1}};
-constexpr int kNumVariants = 11;
+                                   {2, 1, 32, 32, 4},   {8, 2, 32, 32, 4},   {8, 2, 8, 8, SFL_G8_OCC1},
+                                   {2, 1, 32, 32, SFL_LM_OCC, 1}};
+constexpr int kNumVariants = 12;
+// Variant 11 = variant 8 with the map's move table and distance map (as int16) in LDS (LM): a batch of at most two
+// wavefronts per SIMD (kLmWaves; configs[1], c2 at 4,096 envs: 2,048 wavefronts at G = 32) runs two 256-thread blocks
+// per CU, which leaves each block ~63 KB of LDS beyond its env records; the tick's two move-table lookups and the
+// staging's move-table and distance lookups then become LDS reads instead of dependent L2 round trips.  Chosen where
+// the tables fit kLmBytes (c2: 40,000 + 20,000 bytes); SFL_LDS_MAP=0 keeps variant 8.
+constexpr uint64_t kLmWaves = 2048;
+constexpr int64_t kLmBytes = 64512;  // (sfl_wave.h run_groups: LM_WORDS)
+inline int64_t lm_bytes(const sfl_map_desc* md) {
+  const int64_t hw = (int64_t)md->H * md->W;
+  return hw * 4 * 16 + ((int64_t)md->K * hw * 4 + 1) / 2 * 4;
+}
 #ifndef SFL_DEFAULT_G
 #define SFL_DEFAULT_G 16  // lane group size chosen where a grouped shape fits (SFL_WAVE_G overrides)
 #endif
@@ -166,8 +182,18 @@ inline int choose_variant(const sfl_map_desc* md, bool backend_has_wave, std::st
     const WaveShape& w = kVariants[v];
     return md->S * 4 <= w.G * w.PPL && md->S <= w.G * w.SPL && md->T <= w.TW;
   };
-  for (int v = 1; v < kNumVariants; ++v)
-    if (kVariants[v].G == want_g && fits(v)) return v;
+  const char* lms = getenv("SFL_LDS_MAP");
+  const bool lm_ok = !(lms && atoi(lms) == 0) && n_envs > 0 && n_envs * (uint64_t)want_g / 64 <= kLmWaves &&
+                     lm_bytes(md) <= kLmBytes;
+  for (int v = 1; v < kNumVariants; ++v) {
+    if (kVariants[v].LM || kVariants[v].G != want_g || !fits(v)) continue;
+    if (lm_ok)  // the same shape with the map tables in LDS, if there is one
+      for (int u = 1; u < kNumVariants; ++u) {
+        const WaveShape &a = kVariants[u], &b = kVariants[v];
+        if (a.LM && a.PPL == b.PPL && a.SPL == b.SPL && a.TW == b.TW && a.G == b.G) return u;
+      }
+    return v;
+  }
   for (int v = 1; v < kNumVariants; ++v)
     if (kVariants[v].G == 64 && fits(v)) return v;
   return no("more than 256 switches");

@@ -13,10 +13,10 @@
 
 namespace sflk {
 
-template <int PPL, int SPL, int TW, bool TRACE, int G, int OCC, bool TIMED = false>
+template <int PPL, int SPL, int TW, bool TRACE, int G, int OCC, bool TIMED = false, bool LM = false>
 __global__ void __launch_bounds__(SFL_GROUP_BLOCK) __attribute__((amdgpu_waves_per_eu(OCC)))
 k_wave_g(const sfl::SflMap* __restrict__ m, const sfl::SflState* __restrict__ s, const sfl::SflCtl* __restrict__ c) {
-  sfl::wave::run_groups<PPL, SPL, TW, TRACE, G, TIMED>(*m, *s, *c);
+  sfl::wave::run_groups<PPL, SPL, TW, TRACE, G, TIMED, LM>(*m, *s, *c);
 }
 
 // variant 7's three launches (traced, phase-timed, plain): explicit instantiation definitions in

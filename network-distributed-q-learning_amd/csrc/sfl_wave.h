@@ -323,7 +323,8 @@ struct PortRec {
 // their switches' owner ranks, so a decision is observed in one launch (request to the owner) and
 // applied in the next (with the owner's reply), and the post step's Q operations are update
 // records to the owners
-template <int PPL, int SPL, int TWc, bool PART = false, int G = 64>
+// LM (run_groups only, sfl_engine.h variant 11): the map's move table and distance map (int16) live in the block's LDS
+template <int PPL, int SPL, int TWc, bool PART = false, int G = 64, bool LM = false>
 struct WEnv {
   static_assert(G == 64 || G == 32 || G == 16 || G == 8, "lane group of 8, 16, 32 or 64 lanes");
   static_assert(G == 64 || !PART, "the partitioned local step runs one env per wavefront");
@@ -374,6 +375,9 @@ struct WEnv {
   static constexpr int SW_LDS = 12;  // words of a switch record in the block's LDS copy (10 used of sw_pack's 16)
   const uint32_t* tpp = nullptr;
   const uint32_t* tpt = nullptr;
+  // LM: the block's LDS copies of move_tab ([HW][4] rows of 4 words) and of the distance map as int16 pairs (d16)
+  const uint32_t* lmv = nullptr;
+  const uint32_t* ldist = nullptr;
   // this env's semaphore records and switch counters in LDS (one region per wave):
   // uniform reads are broadcast ds_reads, writes one lane's ds_write, and the lane-parallel
   // scans read entries k*64 + lane (conflict-free)
@@ -678,7 +682,18 @@ struct WEnv {
   template <bool UNI>
   __device__ __forceinline__ Move check_action(uint32_t a, int cell, int dir) const {
     const uint32_t i = ((uint32_t)cell * 4u + (uint32_t)dir) * 4u + (a & 3u);
-    return unpack_move(UNI ? LDC(m.move_tab, i) : ld(m.move_tab, i));
+    if constexpr (LM) return unpack_move(lmv[i]);
+    else return unpack_move(UNI ? LDC(m.move_tab, i) : ld(m.move_tab, i));
+  }
+  // the move-table row (all four rail actions) of (cell, dir) = cd, per lane
+  __device__ __forceinline__ u4 move_row(uint32_t cd) const {
+    if constexpr (LM) return *(const u4*)(lmv + 4u * cd);
+    else return ld((const u4*)m.move_tab, (size_t)cd);
+  }
+  // distance-map entry i (int32 semantics: DIST_INF for unreachable)
+  __device__ __forceinline__ int32_t dist_at(uint32_t i, bool uni) const {
+    if constexpr (LM) return d16_lo(ldist[i >> 1] >> (16u * (i & 1u)));
+    else return uni ? LDC(m.dist, i) : ld(m.dist, i);
   }
   template <bool UNI>
   __device__ __forceinline__ bool action_ok(uint32_t a, int cell, int dir) const {
@@ -691,7 +706,7 @@ struct WEnv {
       lerr |= E_INF_DIST;
       return 0;
     }
-    const int32_t d = LDC(m.dist, ((uint32_t)k * (uint32_t)m.HW + (uint32_t)cell) * 4u + (uint32_t)dir);
+    const int32_t d = dist_at(((uint32_t)k * (uint32_t)m.HW + (uint32_t)cell) * 4u + (uint32_t)dir, true);
     if (d >= DIST_INF) lerr |= E_INF_DIST;
     return d;
   }
@@ -706,7 +721,7 @@ struct WEnv {
     pd = go ? mv.dir : pd;
   }
   __device__ __forceinline__ int32_t dist_v(int k, int cell, int dir) const {
-    const int32_t d = ld(m.dist, ((uint32_t)k * (uint32_t)m.HW + (uint32_t)(cell >= 0 ? cell : 0)) * 4u + (uint32_t)dir);
+    const int32_t d = dist_at(((uint32_t)k * (uint32_t)m.HW + (uint32_t)(cell >= 0 ? cell : 0)) * 4u + (uint32_t)dir, false);
     return cell < 0 ? PF_OFFGRID : d;
   }
   // distance staged by prefetch (dist() semantics: off the grid or unreachable sets E_INF_DIST)
@@ -1179,7 +1194,7 @@ struct WEnv {
       const bool ok = mine_(k);
       const int pc = pos[k] >= 0 ? pos[k] : tt1[k][0];
       const int pd = pos[k] >= 0 ? (int)tb_dir(bits[k]) : (int)((uint32_t)tt1[k][3] & 0xFFu);
-      mrows[k] = ld((const u4*)m.move_tab, (size_t)((uint32_t)(ok ? pc : 0) * 4u + (uint32_t)(ok ? pd : 0)));
+      mrows[k] = move_row((uint32_t)(ok ? pc : 0) * 4u + (uint32_t)(ok ? pd : 0));
     }
     bool mover[TPL];
     int32_t desired[TPL], pred[TPL];
@@ -1578,7 +1593,7 @@ struct WEnv {
     const uint32_t n_plan = pl_len(plan_k);
     const uint32_t a1 = n_plan ? pl_front(plan_k) : A_FWD;
     // move-table rows (all four rail actions) at the cell and after the first rail action
-    const u4 row0 = ld((const u4*)m.move_tab, (size_t)((uint32_t)pos0 * 4u + (uint32_t)dir0));
+    const u4 row0 = move_row((uint32_t)pos0 * 4u + (uint32_t)dir0);
     auto mv_in = [](const u4& r, uint32_t a) -> Move {
       const uint32_t q = a & 3u;
       return unpack_move(q == 0 ? r[0] : q == 1 ? r[1] : q == 2 ? r[2] : r[3]);
@@ -2579,9 +2594,9 @@ __device__ void run(const SflMap& m, const SflState& s, const SflCtl& c, const S
 // follow it -- as a flat loop in which each iteration advances every group by at most one tick,
 // one post step and one decision.  The groups of a wave diverge (one ticks while another decides);
 // a batch loop as in run() would hold every group until the longest batch of the wave is done.
-template <int PPL, int SPL, int TW, bool TRACE, int G, bool TIMED = false>
+template <int PPL, int SPL, int TW, bool TRACE, int G, bool TIMED = false, bool LM = false>
 __device__ void run_groups(const SflMap& m, const SflState& s, const SflCtl& c) {
-  using V = WEnv<PPL, SPL, TW, false, G>;
+  using V = WEnv<PPL, SPL, TW, false, G, LM>;
   // per env: semaphores, counters, prefetch records, rng; per block: the timetable rows and the
   // per-switch / per-port map records (the groups of a wave read different switches' records: LDS
   // reads instead of vector loads)
@@ -2589,12 +2604,24 @@ __device__ void run_groups(const SflMap& m, const SflState& s, const SflCtl& c) 
   constexpr int EPB = SFL_GROUP_BLOCK / G;  // envs per block (sfl.hip launches)
   constexpr int SWX = G * SPL, NPX = G * PPL;  // switches / ports the shape holds
   constexpr int O_TT = EPB * LDS_WORDS, O_SW = O_TT + TW * 8, O_PP = O_SW + SWX * V::SW_LDS, O_PT = O_PP + NPX * 4;
-  __shared__ __attribute__((aligned(16))) uint32_t lds[O_PT + NPX * 4];
+  // LM: the move table and the distance map (int16 pairs) after the map records, within 64,512 bytes
+  // (sfl_engine.h kLmBytes: two such blocks fill the CU's LDS)
+  constexpr int O_LM = O_PT + NPX * 4, LM_WORDS = LM ? 16128 : 0;
+  __shared__ __attribute__((aligned(16))) uint32_t lds[O_LM + LM_WORDS];
   for (int i = (int)threadIdx.x; i < m.S * V::SW_LDS; i += (int)blockDim.x)
     lds[O_SW + i] = m.sw_pack[(i / V::SW_LDS) * 16 + i % V::SW_LDS];
   for (int i = (int)threadIdx.x; i < m.NP * 4; i += (int)blockDim.x) {
     lds[O_PP + i] = m.port_pack[i];
     lds[O_PT + i] = m.port_tr[i];
+  }
+  const int lm_mv = LM ? m.HW * 16 : 0;  // move-table words
+  if constexpr (LM) {
+    const int nd = m.K * m.HW * 4;  // distance entries
+    for (int i = (int)threadIdx.x; i < lm_mv; i += (int)blockDim.x) lds[O_LM + i] = m.move_tab[i];
+    for (int j = (int)threadIdx.x; 2 * j < nd; j += (int)blockDim.x) {
+      const uint32_t lo = d16(m.dist[2 * j]), hi = 2 * j + 1 < nd ? d16(m.dist[2 * j + 1]) : 0u;
+      lds[O_LM + lm_mv + j] = lo | (hi << 16);
+    }
   }
   __syncthreads();
   const uint32_t e = (uint32_t)((blockIdx.x * blockDim.x + threadIdx.x) / G);
@@ -2603,6 +2630,10 @@ __device__ void run_groups(const SflMap& m, const SflState& s, const SflCtl& c) 
   v.tsw = lds + O_SW;
   v.tpp = lds + O_PP;
   v.tpt = lds + O_PT;
+  if constexpr (LM) {
+    v.lmv = lds + O_LM;
+    v.ldist = lds + O_LM + lm_mv;
+  }
   PhaseTimer tm;
   if constexpr (TIMED) tm.start(c.phase_cyc != nullptr && blockIdx.x % TM_SAMPLE == 0u && threadIdx.x < 64u);
   v.load();

@@ -19,6 +19,7 @@
 #   c5fused    c5 fused at 16,384 envs
 #   part       the 8-rank partition rehearsal on one GPU (with the env-sharded fused comparison)
 #   ab         bench for each library in LIBS (SFL_LIB, --experimental for all but libsfl)
+#   abenv      bench of the product library for each runtime setting in ABENV (e.g. "SFL_LDS_MAP=1 SFL_LDS_MAP=0")
 #   eval       the published evaluation table (scripts/eval_table.py) through libsfl.so, 15 trains
 #   eval100    one 100-train learning run + greedy evaluation through libsfl.so (SEEDS100, default 66)
 set -o pipefail
@@ -111,6 +112,14 @@ for S in "$@"; do
         line $OUT/ab_${i}_${L}.json
       done
       unset SFL_LIB ;;
+    abenv)  # the product library under each runtime setting in ABENV (e.g. "SFL_LDS_MAP=1 SFL_LDS_MAP=0"), BENCH_ARGS
+      i=0
+      for E in ${ABENV}; do
+        i=$((i+1))
+        N=$(echo $E | tr '=' '_')
+        env $E timeout -k 10 300 python bench.py --steps ${STEPS:-10} --warmup 2 --no-cpu --sustain-seconds 0 ${BENCH_ARGS} > $OUT/abenv_${i}_${N}.json 2> $OUT/abenv_${i}_${N}.err; ok $? "abenv $E"
+        line $OUT/abenv_${i}_${N}.json
+      done ;;
     eval)  # the 15-train sweep config with malfunctions, 3 seeds x 10 evaluations, vs the host build's run
       timeout -k 10 900 python -u scripts/eval_table.py $OUT/eval_table.json --compare profiles/r06_eval_table_host.json ${EVAL_ARGS} > $OUT/eval_table.log 2>&1; rc=$?
       grep -v "^\.\.\." $OUT/eval_table.log | tail -6; ok $rc "eval" ;;

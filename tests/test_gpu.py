@@ -464,6 +464,33 @@ def test_c2_stated_batch_4096(lib):
     bh.close()
 
 
+@pytest.mark.parametrize("lds_map", ["1", "0"])
+def test_c2_stated_batch_lds_map_variant(lib, monkeypatch, lds_map):
+    """configs[1]'s batch runs variant 11 (variant 8 with the move table and distance map in LDS, sfl_engine.h); with
+    SFL_LDS_MAP=0 variant 8 reads them from global memory.  Both bit-equal to the host build on 512 of its envs (the
+    same 2,048-wavefront launch shape: the other envs run too)."""
+    from tests import hostsim
+    monkeypatch.setenv("SFL_LDS_MAP", lds_map)
+    monkeypatch.delenv("SFL_WAVE_G", raising=False)
+    cm = comp.compile_scenario(mapgen.make_config("c2"))
+    seeds = [777 + i for i in range(4096)]
+    bg = runtime.Batch(cm, HP, seeds, lib=lib)
+    assert bg.counters()["kernel_variant"] == (11 if lds_map == "1" else 8)
+    pick = list(range(0, 4096, 8))
+    bh = runtime.Batch(cm, HP, [seeds[e] for e in pick], lib=hostsim.lib())
+    for b in (bg, bh):
+        b.learn_begin()
+        b.apply_qinit()
+        for n in (300, 700):
+            b.step(n)
+    for i, e in enumerate(pick):
+        qg, tg = bg.q_raw(e)
+        qh, th = bh.q_raw(i)
+        assert np.array_equal(qg, qh) and np.array_equal(tg, th), f"env {e}"
+    bg.close()
+    bh.close()
+
+
 def test_device_pow_beyond_tables(lib, kernel):
     """ntab = 16: epsilon beyond the host table comes from the device's pow (pow_ool); checked
     against the oracle's Python ``**`` (distr_q.py:59-68) bit-exactly.  (eps only decides
