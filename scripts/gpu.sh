@@ -19,6 +19,7 @@
 #   c5fused    c5 fused at 16,384 envs
 #   part       the 8-rank partition rehearsal on one GPU (with the env-sharded fused comparison)
 #   ab         bench for each library in LIBS (SFL_LIB, --experimental for all but libsfl)
+#   rehearse   bench.py --gpus 2 / 4 (REH_N) as gloo ranks sharing this GPU: launcher, sharding, parity, the leg
 #   abenv      bench of the product library for each runtime setting in ABENV (e.g. "SFL_LDS_MAP=1 SFL_LDS_MAP=0")
 #   eval       the published evaluation table (scripts/eval_table.py) through libsfl.so, 15 trains
 #   eval100    one 100-train learning run + greedy evaluation through libsfl.so (SEEDS100, default 66)
@@ -112,6 +113,12 @@ for S in "$@"; do
         line $OUT/ab_${i}_${L}.json
       done
       unset SFL_LIB ;;
+    rehearse)  # the N > 1 bench path on this one GPU: REH_N gloo ranks sharing device 0 (not the RCCL transport)
+      for N in ${REH_N:-2 4}; do
+        SFL_DIST_BACKEND=gloo SFL_DEVICE=0 timeout -k 10 600 python bench.py --gpus $N --envs 8192 --steps 3 --warmup 1 > $OUT/gpus$N.json 2> $OUT/gpus$N.err; rc=$?
+        [ $rc -eq 0 ] || tail -5 $OUT/gpus$N.err; ok $rc "rehearse --gpus $N"
+        python -c "import json;d=json.loads([l for l in open('$OUT/gpus$N.json') if l.startswith('{')][0]);L=d.get('partition_leg') or {};print('  world %d %s %.1fM/s parity %s (%d envs, %d threads/rank); leg %s parity %s vs fused %s' % (d['world_size'], d['backend'], d['value']/1e6, d['parity'], d['parity_envs_checked'], d['parity_threads_per_rank'], L.get('value'), L.get('parity'), L.get('vs_env_sharded_fused')))"
+      done ;;
     abenv)  # the product library under each runtime setting in ABENV (e.g. "SFL_LDS_MAP=1 SFL_LDS_MAP=0"), BENCH_ARGS
       i=0
       for E in ${ABENV}; do
