@@ -180,10 +180,12 @@ class OraclePool:
             for _ in self.procs:
                 self.jobs.put(None)
             self.used = True
+        deadline = time.monotonic() + 30.0  # (one budget for all: a worker may be stuck behind a dead one's queue lock)
         for p in self.procs:
-            p.join(timeout=30)
+            p.join(timeout=max(0.0, deadline - time.monotonic()))
+        for p in self.procs:
             if p.exitcode is None:
-                p.kill()
+                p.kill()  # (this pool's own child, by its handle)
                 p.join(timeout=5)
 
     def join(self):
