@@ -243,6 +243,19 @@ def cpu_oracle_baseline(config: str, seconds: float, pool=None, check=None):
     return out
 
 
+JSON_OUT = [sys.stdout]
+
+
+def json_stdout():
+    """Keep stdout for the one JSON line: from here on everything else written to file descriptor 1 -- RCCL's version
+    banner at communicator set-up, gloo's connection lines, library or Python prints -- goes to stderr, and the
+    line is written to a duplicate of the original stdout (JSON_OUT)."""
+    sys.stdout.flush()
+    fd = os.dup(1)
+    os.dup2(2, 1)
+    JSON_OUT[0] = os.fdopen(fd, "w", buffering=1)
+
+
 def visible_gpus() -> int:
     """GPUs this process may use, counted without any HIP call: the KFD topology's GPU nodes (gpu_id != 0),
     restricted by ROCR_VISIBLE_DEVICES / HIP_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES when set."""
@@ -442,6 +455,9 @@ def main():
     ap.add_argument("--partition", action="store_true",
                     help="graph-partitioned mode (BASELINE configs[4]): switch agents owned by ranks, RCCL all-to-all "
                          "of row lookups and updates; defaults to --config c5 --envs 16384 (238 GB of owned Q rows per GPU)")
+    ap.add_argument("--rccl-one-rank", action="store_true",
+                    help="--partition on one GPU: the segments still travel as RCCL all-to-alls (a process group of "
+                         "one) -- RCCL's cost inside the round, which a single-rank job otherwise skips")
     ap.add_argument("--rehearse-on-host", action="store_true",
                     help="TEST ONLY: run the ranks on the host build of the kernel body (libsfl_hostsim.so, gloo) to "
                          "rehearse the launcher without a GPU; the line says so and is no measurement")
@@ -449,6 +465,7 @@ def main():
     rc = launch_or_check(args, sys.argv[1:])
     if rc is not None:
         sys.exit(rc)
+    json_stdout()
     if args.experimental:
         os.environ["SFL_EXPERIMENTAL"] = "1"
     if args.partition:
@@ -594,7 +611,7 @@ def main():
     def emit(r):
         if not printed:
             printed.append(1)
-            print(json.dumps(r), flush=True)
+            print(json.dumps(r), file=JSON_OUT[0], flush=True)
     if world > 1 and os.environ.get("SFL_NO_PARTITION_LEG") != "1":
         leg = partition_leg(par, dist, world, rank, dev, red_dev, devices, res, emit, host=host)
         if rank == 0:
@@ -616,6 +633,16 @@ def bench_partition(args):
     dist, dev, red_dev = dist_setup(par, local, host)
     if not host:
         torch.cuda.set_device(dev)
+    if getattr(args, "rccl_one_rank", False) and world == 1 and not host:
+        # one rank whose segments still travel as RCCL collectives (partition.PartitionedBatch exchange_collective):
+        # RCCL's launch and stream costs inside the round, measured on one GPU
+        import torch.distributed as tdist
+        s_ = socket.socket()
+        s_.bind(("127.0.0.1", 0))
+        port = s_.getsockname()[1]
+        s_.close()
+        tdist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", world_size=1, rank=0)
+        dist, red_dev = tdist, "cuda"
     devices = rank_devices(dist, -1 if host else dev, device=red_dev)
     if rank == 0:
         build = importlib.import_module(PKG + ".build")
@@ -624,7 +651,7 @@ def bench_partition(args):
         dist.barrier()
     res = partition_run(args, par, dist, world, rank, dev, red_dev, devices, host=host)
     if rank == 0:
-        print(json.dumps(res), flush=True)
+        print(json.dumps(res), file=JSON_OUT[0], flush=True)
     if dist is not None:
         dist.destroy_process_group()
 
@@ -656,7 +683,8 @@ def partition_run(args, par, dist, world, rank, dev, red_dev, devices, host: boo
     # default: one cohort on the host build and on an RCCL job of several ranks (each cohort has its own
     # communicator, and concurrent communicators on one device have not been run on RCCL yet); --cohorts N asks
     # for the pipeline anyway
-    rccl_multi = world > 1 and dist is not None and dist.get_backend() == "nccl"
+    rccl_multi = ((world > 1 or getattr(args, "rccl_one_rank", False)) and dist is not None
+                  and dist.get_backend() == "nccl")
     cohorts = min(E, cohorts if cohorts else (1 if (host or rccl_multi) else PARTITION_COHORTS))
     # the break-even comparison: the same envs run env-sharded on the fused kernel -- every rank its
     # own envs with all their Q rows, no exchange -- timed the same way, before the partitioned job allocates
@@ -685,6 +713,8 @@ def partition_run(args, par, dist, world, rank, dev, red_dev, devices, host: boo
         fb.close()
     kw = dict(rank=rank, world=world, dist=dist, device=dev, lib=lib, buffer_device="cpu" if host else "cuda",
               local_rows=local)
+    if getattr(args, "rccl_one_rank", False) and world == 1 and dist is not None:
+        kw["exchange_collective"] = True
     pb = (part.CohortPipeline(cm, HP, seeds, rank * E, world * E, cohorts=cohorts, **kw) if cohorts > 1
           else part.PartitionedBatch(cm, HP, seeds, rank * E, world * E, **kw))
     pb.learn_begin()
@@ -751,7 +781,10 @@ def partition_run(args, par, dist, world, rank, dev, red_dev, devices, host: boo
                        "host_waits_per_step": (w1 - w0) / max(1, args.steps),
                        "count_reads_per_step": (r1 - r0) / max(1, args.steps),
                        "segment_records": pb.k_msg, "segment_capacity": pb.cap_msg,
-                       "collectives_per_round": 2 if world > 1 else 0,
+                       "collectives_per_round": 2 if (world > 1 or kw.get("exchange_collective")) else 0,
+                       "exchange": ("RCCL all_to_all_single" if (dist is not None and dist.get_backend() == "nccl"
+                                                                 and (world > 1 or kw.get("exchange_collective")))
+                                    else "gloo all_to_all_single" if world > 1 else "identity (one rank)"),
                        "cohorts": cohorts,
                        "deferrals": pb.deferrals - d0,
                        "parallelism": f"env-batch dp{world} x switch-agent partition {world}"},

@@ -89,7 +89,7 @@ class PartitionedBatch:
                  owner: Optional[np.ndarray] = None, upd_per_env: int = 16, ntab: Optional[int] = None,
                  buffer_device: str = "cuda", local_rows=True, malfunction_stream: str = "counter",
                  delay_threshold: int = 20, k_init: Optional[int] = None, checkpoint_every_round: bool = False,
-                 group=None):
+                 group=None, exchange_collective: bool = False):
         import torch
         self.torch = torch
         kw = {} if ntab is None else dict(ntab=ntab)
@@ -99,6 +99,9 @@ class PartitionedBatch:
         self.lib = self.batch.lib
         self.cm, self.rank, self.world, self.dist = cm, int(rank), int(world), dist
         self.group = group  # the process group of this job's collectives (None: the default group)
+        # (tests) with one rank too, exchange the segments as collectives of `dist` between separate send and receive
+        # buffers -- with RCCL, the same stream ordering as a multi-GPU job's, on one GPU
+        self.exchange_collective = bool(exchange_collective) and dist is not None
         self.E = self.batch.E
         self.env_base, self.envs_total = int(env_base), int(envs_total)
         self.owner = np.ascontiguousarray(owner if owner is not None else partition_switches(cm, world), np.int32)
@@ -122,7 +125,7 @@ class PartitionedBatch:
         nmsg = self.world * (self.cap_msg + 1) * ms.value
         nrep = self.world * (self.cap_msg + 1) * rp.value
         z = lambda n: torch.zeros(n, dtype=torch.uint8, device=dev)  # noqa: E731
-        if self.world == 1:
+        if self.world == 1 and not self.exchange_collective:
             # one rank: every segment is addressed to this rank, so the exchange is the identity
             # and each receive buffer is its send buffer (no copies, no stream synchronisation)
             self.msg_send = self.msg_recv = z(nmsg)
@@ -225,7 +228,7 @@ class PartitionedBatch:
         """Fixed-size all-to-all of the [world][k + 1]-record segments (RCCL device to device; gloo with
         device buffers stages them through host memory)."""
         r, s_ = self._view(recv, k, rec), self._view(send, k, rec)
-        if self.world == 1:
+        if self.world == 1 and not self.exchange_collective:
             if r.data_ptr() != s_.data_ptr():
                 r.copy_(s_)
             return

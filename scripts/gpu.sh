@@ -18,6 +18,7 @@
 #   c2big      c2 at 65,536 envs
 #   c5fused    c5 fused at 16,384 envs
 #   part       the 8-rank partition rehearsal on one GPU (with the env-sharded fused comparison)
+#   partrccl   the same with the segments exchanged by RCCL all-to-alls of a one-rank group
 #   ab         bench for each library in LIBS (SFL_LIB, --experimental for all but libsfl)
 #   rehearse   bench.py --gpus 2 / 4 (REH_N) as gloo ranks sharing this GPU: launcher, sharding, parity, the leg
 #   abenv      bench of the product library for each runtime setting in ABENV (e.g. "SFL_LDS_MAP=1 SFL_LDS_MAP=0")
@@ -103,6 +104,11 @@ for S in "$@"; do
       [ $rc -eq 0 ] || tail -5 $OUT/part.err; ok $rc "part"
       line $OUT/part.json
       python -c "import json;d=json.load(open('$OUT/part.json'));print('  fused env-sharded %.1fM/s, vs_env_sharded_fused %.3f' % (d['env_sharded_fused']['value']/1e6, d['vs_env_sharded_fused']))" ;;
+    partrccl)  # the partition rehearsal with its segments as RCCL collectives of a one-rank group (RCCL's round cost)
+      timeout -k 10 400 python bench.py --partition --steps 3 --warmup 1 --decisions 1024 --virtual-ranks 8 --verify-envs 4 --rccl-one-rank ${PART_ARGS} > $OUT/part_rccl.json 2> $OUT/part_rccl.err; rc=$?
+      [ $rc -eq 0 ] || tail -5 $OUT/part_rccl.err; ok $rc "part rccl"
+      line $OUT/part_rccl.json
+      python -c "import json;d=json.load(open('$OUT/part_rccl.json'));c=d['config'];print('  exchange %s, %s collectives/round, %.1f rounds/step, cohorts %s' % (c['exchange'], c['collectives_per_round'], c['rounds_per_step'], c['cohorts']))" ;;
     ab)
       i=0
       for L in ${LIBS:-libsfl}; do

@@ -34,6 +34,8 @@ def test_gpus_2_launches_two_ranks_end_to_end():
     assert "launching" in r.stderr and "--nproc-per-node=2" in r.stderr
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout  # rank 0 only
+    # stdout is the JSON line and nothing else (gloo's / RCCL's own prints go to stderr, bench.json_stdout)
+    assert r.stdout.strip().splitlines() == lines, r.stdout[:2000]
     res = json.loads(lines[0])
     assert res["n_gpus"] == 2 and res["world_size"] == 2 and res["backend"] == "gloo"
     assert res["devices"] == [-1, -1]

@@ -338,6 +338,17 @@ def test_two_rank_partition_gpu_rounds_queue_between_checkpoints(lib):
         assert s["reads"] == s["checkpoints"] <= 8 + s["rounds"] // 32
 
 
+def test_partition_rccl_one_rank_stream_ordering(lib):
+    """RCCL itself on the partitioned exchange: one rank over backend "nccl" whose segments still travel as
+    all_to_all_single collectives between separate device buffers, queued on the job's stream between the wave
+    kernel's local step and the owner kernel -- the stream ordering of a multi-GPU job (RCCL refuses two ranks on
+    one GPU).  A missing dependency would let the owner read stale messages; owned rows and env states equal the
+    fused host run."""
+    from tests import test_partition
+    rounds = test_partition.one_rank_collective_run("nccl")
+    assert all(r > 1 for r in rounds)
+
+
 def test_two_rank_partition_gpu_deferred_envs_bit_equal(lib):
     """k_part_compact's deferral on the device: segments of 2 message records per destination to start with,
     envs deferred whole and skipped by the wave kernel's local step until they fit."""

@@ -264,6 +264,64 @@ def test_cohort_shortage_on_one_rank_raises_on_every_rank():
     assert res == [(0, "ValueError"), (1, "ValueError")], res
 
 
+def _one_rank_collective_worker(port, backend, q, cfg="c5", steps=(40, 75, 600)):
+    """One rank whose segments still travel as collectives of `backend` (PartitionedBatch(exchange_collective=True)):
+    with RCCL on the GPU this is the stream ordering of a multi-GPU job -- local step, all_to_all_single, owner step,
+    all_to_all_single, all queued on the job's stream -- on one device (RCCL refuses two ranks on one GPU).  Rows of
+    block 0 of a 4-rank partition stay local, the rest travel as messages; owned rows and env states must equal the
+    fused host run."""
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+        import torch
+        import torch.distributed as dist
+        if backend == "nccl":
+            torch.cuda.set_device(0)
+        dist.init_process_group(backend)  # (a group of one: parallel.init returns None for one rank)
+        cm = comp.compile_scenario(mapgen.make_config(cfg))
+        E = 6
+        seeds = [450565 + i for i in range(E)]
+        if backend == "nccl":
+            lib = importlib.import_module("network-distributed-q-learning_amd._lib").load_product()
+            kw = dict(lib=lib, device=0, buffer_device="cuda")
+        else:
+            kw = dict(lib=hostsim.lib(), buffer_device="cpu")
+        loc = (part.partition_switches(cm, 4) == 0).astype(np.uint8)
+        pb = part.PartitionedBatch(cm, HP, seeds, 0, E, dist=dist, ntab=4096, local_rows=loc, exchange_collective=True,
+                                   **kw)
+        assert pb.msg_send.data_ptr() != pb.msg_recv.data_ptr()
+        pb.learn_begin()
+        pb.apply_qinit()
+        rounds = [pb.step(n) for n in steps]
+        if backend == "nccl":
+            torch.cuda.synchronize()
+        _check_rank(pb, _fused(cm, seeds, steps), range(E))
+        pb.close()
+        dist.destroy_process_group()
+        q.put(("ok", rounds, backend))
+    except Exception as ex:  # report to the parent instead of hanging it
+        import traceback
+        q.put((repr(ex), traceback.format_exc()[-2000:], backend))
+        raise
+
+
+def one_rank_collective_run(backend):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_one_rank_collective_worker, args=(_free_port(), backend, q))
+    p.start()
+    res = q.get(timeout=600)
+    p.join(timeout=120)
+    assert res[0] == "ok", res
+    assert p.exitcode == 0
+    return res[1]
+
+
+def test_one_rank_collective_exchange_matches_fused():
+    """The exchange as gloo collectives between separate buffers on one rank (the GPU twin runs it on RCCL)."""
+    rounds = one_rank_collective_run("gloo")
+    assert all(r > 1 for r in rounds)  # (messages: 3/4 of the switches are another block's)
+
+
 def test_two_rank_1024_decision_step_syncs_only_at_checkpoints():
     """Two gloo ranks, one 1,024-decision step: the rounds between checkpoints run without the host
     reading a count (fixed-size segments; the ranks agree on their size at the checkpoints), the
