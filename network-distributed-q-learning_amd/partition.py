@@ -388,6 +388,10 @@ class CohortPipeline:
         E, C_ = len(seeds), int(cohorts)
         if C_ < 1:
             raise ValueError(f"CohortPipeline: {C_} cohorts")
+        if kw.get("exchange_collective") and int(world) == 1 and C_ > 1:
+            # (one rank has no per-cohort process groups: the cohorts' collectives would share one communicator
+            # from several streams)
+            raise ValueError("CohortPipeline: exchange_collective with one rank needs cohorts=1")
         self.cm, self.rank, self.world, self.dist = cm, int(rank), int(world), dist
         self.E, self.env_base, self.envs_total, self.cohorts = E, int(env_base), int(envs_total), C_
         # every rank's env count (its cohorts' sizes follow from it)
