@@ -31,8 +31,11 @@ namespace wave {
 // of 10 fits four 16-env blocks per CU (40.4 KB each), and 4 waves per SIMD then have to live in
 // 128 VGPRs: with the env's Q / key-set / slot base pointers held in registers 86 spilled (c3
 // 1,097 M vs 1,308 M at 3 waves); recomputed from the env index at each use (qbase / tbase /
-// sbase) 57, mostly in the episode-end bookkeeping: 1,351 M vs 1,298 M (3 waves, no ring)
-#define SFL_PF_RING 10
+// sbase) 57, mostly in the episode-end bookkeeping: 1,351 M vs 1,298 M (3 waves, no ring).  Round 6: 12 -- the
+// largest ring that still fits four blocks per CU (40,448 B per block; up to 16 records the staged offsets stay one
+// register per lane) -- c3 1,640-1,644 M vs 1,611-1,615 M for 10, +1.8 %; 11: 1,558 M, 8: 1,576 M
+// (profiles/r06p_pf_ring_ab.txt)
+#define SFL_PF_RING 12
 #endif
 #ifndef SFL_PF_RING64
 #define SFL_PF_RING64 16  // one env per wavefront with two train slots per lane (c5, k_wave2): see WEnv::RING
